@@ -1,0 +1,229 @@
+/*
+ * htm_amd.h -- C ABI of the MI355X-native batched HTM engine.
+ *
+ * One engine = N independent metric streams, each a Model-1 network
+ * (ScalarEncoder -> SpatialPooler -> BacktrackingTM -> raw anomaly), stepped
+ * in lockstep on one GPU.  Plain pointers and sizes only; no C++ exceptions
+ * cross this boundary; every entry point returns 0 on success or a negative
+ * HTM_E* code, with htm_last_error() describing the failure.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repo root; NuPIC symbols are the external library the reference
+ * calls):
+ *   htm_create        Network() + addRegion(RecordSensor/SPRegion/TMRegion)
+ *                     + link(): ML/HTM/NetworkModel.py:48-110,
+ *                     ML/HTM/NetworkUtils.py:111-153 (params :25-64, :77-88)
+ *   htm_set_learning  region.setParameter("learningMode", b):
+ *                     ML/HTM/NetworkUtils.py:132,147, ML/HTM/NetworkModel.py:40-44
+ *                     (SP and TM flags are independent: the reference keeps
+ *                     SP learning on while TM learning is off)
+ *   htm_step          dataSource.setData(v) + network.run(1) +
+ *                     getOutputData("anomalyScore")[0]:
+ *                     ML/HTM/NetworkModel.py:35-46,112-133,
+ *                     ML/HTM/StreamReader.py:157-161
+ *   htm_get_output    region.getOutputData(...): NetworkModel.py:129,133
+ *   htm_save/htm_load network.save(path) / Network(path):
+ *                     ML/HTM/NetworkUtils.py:156-163, ModelTesting.py:176
+ *   htm_reset_tm      TMRegion resetIn -> BacktrackingTM.reset() [ext]
+ *   htm_last_error    NTA_THROW -> RuntimeError convention [ext]
+ */
+#ifndef HTM_AMD_H
+#define HTM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HTM_ABI_VERSION 1
+
+/* error codes */
+#define HTM_OK 0
+#define HTM_E_INVALID (-1)   /* bad argument / unsupported parameter */
+#define HTM_E_HIP (-2)       /* HIP runtime failure */
+#define HTM_E_CAPACITY (-3)  /* a per-stream pool overflowed (see last_error) */
+#define HTM_E_IO (-4)        /* save/load failure */
+#define HTM_E_STATE (-5)     /* call not valid in the current engine state */
+
+/* Network parameters of one stream.  Field meaning, units and defaults are
+ * the reference's (htm_default_config): encoder NetworkUtils.py:77-88,
+ * SP_PARAMS NetworkUtils.py:26-41, TM_PARAMS NetworkUtils.py:44-64, plus the
+ * NuPIC defaults the reference relies on. */
+typedef struct {
+    /* ScalarEncoder per field (MultiEncoder: fields in sorted name order) */
+    int32_t n_fields;            /* 1 (Model 1: cpu) .. 4 */
+    int32_t enc_n;               /* 500 */
+    int32_t enc_w;               /* 21 */
+    double enc_minval;           /* 0.0 */
+    double enc_maxval;           /* 100.0 */
+    int32_t enc_clip;            /* 1 */
+    /* SpatialPooler */
+    int32_t sp_columns;          /* 2048 (multiple of 64, <= 4096) */
+    int32_t sp_num_active;       /* 40 (<= 64) */
+    float sp_potential_pct;      /* 0.8 */
+    float sp_perm_connected;     /* 0.1 */
+    float sp_perm_active_inc;    /* 0.0001 */
+    float sp_perm_inactive_dec;  /* 0.0005 */
+    float sp_min_pct_overlap_dc; /* 0.001 */
+    int32_t sp_duty_cycle_period;/* 1000 */
+    float sp_boost_strength;     /* 0.0 (only 0 is supported: boost == 1) */
+    int32_t sp_stimulus_threshold; /* 0 */
+    int32_t sp_update_period;    /* 50 */
+    uint64_t sp_seed;            /* 2045 */
+    /* BacktrackingTM */
+    int32_t tm_cells_per_col;    /* 12 (<= 32) */
+    int32_t tm_new_syn_count;    /* 20 (<= 32) */
+    int32_t tm_max_syn_per_seg;  /* 32 (<= 32) */
+    int32_t tm_max_segs_per_cell;/* 128 (<= 255) */
+    float tm_initial_perm;       /* 0.21 */
+    float tm_connected_perm;     /* 0.5 */
+    float tm_perm_inc;           /* 0.1 */
+    float tm_perm_dec;           /* 0.1 */
+    float tm_perm_max;           /* 1.0 */
+    int32_t tm_min_threshold;    /* 9 */
+    int32_t tm_activation_threshold; /* 12 */
+    int32_t tm_pam_length;       /* 3 */
+    int32_t tm_max_inf_backtrack;/* 10 (<= 15) */
+    int32_t tm_max_lrn_backtrack;/* 5 (<= 15) */
+    int32_t tm_max_seq_length;   /* 32 */
+    int32_t tm_seg_update_valid_duration; /* 5 */
+    uint64_t tm_seed;            /* 2045 */
+    /* engine capacities (per stream) */
+    int32_t seg_capacity;        /* segment pool slots per stream */
+    int32_t upd_capacity;        /* queued segment updates per stream */
+    int32_t seed_stride;         /* stream s uses seeds sp_seed + s*stride,
+                                    tm_seed + s*stride (0: all identical) */
+} htm_config;
+
+typedef struct htm_engine htm_engine;
+
+/* Fill *cfg with the reference's Model-1 parameters. */
+void htm_default_config(htm_config* cfg);
+
+/* Create an engine of n_streams streams on HIP device `device`, running
+ * the NuPIC initialisation (SP potential pools / permanences from
+ * nupic::Random(seed)) on the GPU.  *out receives the handle. */
+int htm_create(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out);
+int htm_destroy(htm_engine* eng);
+
+/* Independent SP / TM learning flags (both start on, like the regions). */
+int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
+
+/* Engine options. */
+#define HTM_OPT_FROZEN_INDEX 1 /* 1 (default): while TM learning is off, infer through the
+                                  frozen cell->segment forward index; 0: scan the pool */
+#define HTM_OPT_KEEP_PREV 2    /* 1: retain prevPredictedColumns for HTM_OUT_PREV_PRED_COLS */
+#define HTM_OPT_KEEP_OVERLAPS 3 /* 1: retain SP overlaps for HTM_OUT_SP_OVERLAPS */
+int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
+
+/* Synchronise and check every stream's overflow flags (HTM_E_CAPACITY). */
+int htm_status(htm_engine* eng);
+
+/* One network.run(1) for every stream.  d_values: device pointer to
+ * n_streams * n_fields doubles (NaN = missing value).  d_scores: device
+ * pointer to n_streams floats receiving the raw anomaly score.  stream: a
+ * hipStream_t (NULL = default stream).  Asynchronous w.r.t. the host. */
+int htm_step(htm_engine* eng, const double* d_values, float* d_scores, void* stream);
+
+/* Run n_steps steps back to back: d_values is [n_steps][n_streams][n_fields],
+ * d_scores is [n_steps][n_streams]. */
+int htm_run(htm_engine* eng, int32_t n_steps, const double* d_values, float* d_scores, void* stream);
+
+/* Output selectors for htm_get_output (all per stream, concatenated over
+ * streams, written to a DEVICE buffer of `bytes` bytes on `stream`). */
+#define HTM_OUT_ACTIVE_COLUMNS 1   /* uint8 [ncol]  SP bottomUpOut */
+#define HTM_OUT_PREV_PRED_COLS 2   /* uint8 [ncol]  nonzero(colConfidence(t-1)) */
+#define HTM_OUT_INF_ACTIVE 3       /* uint32 bitmap [ncells/32] infActiveState t */
+#define HTM_OUT_INF_PREDICTED 4    /* uint32 bitmap [ncells/32] infPredictedState t */
+#define HTM_OUT_LRN_ACTIVE 5       /* uint32 bitmap [ncells/32] lrnActiveState t */
+#define HTM_OUT_LRN_PREDICTED 6    /* uint32 bitmap [ncells/32] lrnPredictedState t */
+#define HTM_OUT_COL_CONFIDENCE 7   /* float [ncol]  colConfidence t (topDownOut) */
+#define HTM_OUT_TM_OUTPUT 8        /* uint32 bitmap [ncells/32] bottomUpOut = infP|infA */
+#define HTM_OUT_SP_OVERLAPS 9      /* int32 [ncol] SP overlaps of the last step */
+int htm_get_output(htm_engine* eng, int32_t which, void* d_dst, size_t bytes, void* stream);
+/* Bytes per stream of an output selector (0 if unknown). */
+size_t htm_output_bytes(const htm_engine* eng, int32_t which);
+
+/* Raw per-stream state export/import (host buffers), used by save/load and
+ * by the parity tests.  Region ids and layouts are documented in DESIGN.md
+ * §State layout; htm_state_bytes gives the per-stream size of a region. */
+#define HTM_ST_SP_CONNT 1      /* uint32 [nin_pad][ncol/32] connected, input-major */
+#define HTM_ST_SP_POTMASK 2    /* uint32 [ncol][nin_pad/32] potential pool */
+#define HTM_ST_SP_PERM 3       /* float  [ncol][n_potential] potential order */
+#define HTM_ST_SP_DUTY 4       /* float  [2][ncol] overlap, active duty cycles */
+#define HTM_ST_SP_SCALARS 5    /* uint32 [4] iter, iter_learn, min_overlap_dc bits, 0 */
+#define HTM_ST_TM_HEADER 6     /* struct htm_tm_header */
+#define HTM_ST_TM_BITMAPS 7    /* uint32 [4][ncells/32] infA, infP, lrnA, lrnP */
+#define HTM_ST_TM_COLCONF 8    /* float [ncol] */
+#define HTM_ST_TM_SEG_META 9   /* uint32 [seg_capacity] cell | nsyn<<16 | seq<<22 | live<<23 */
+#define HTM_ST_TM_SEG_SRC 10   /* uint16 [seg_capacity][32] */
+#define HTM_ST_TM_SEG_PERM 11  /* float [seg_capacity][32] */
+#define HTM_ST_TM_SEG_CONN 12  /* uint32 [seg_capacity] connected-synapse mask */
+#define HTM_ST_TM_SEG_DUTY 13  /* uint32 [seg_capacity][3] posAct, lastDC bits, lastDCIter */
+#define HTM_ST_TM_CELL_NSEG 14 /* uint8 [ncells] segments per cell */
+#define HTM_ST_TM_PATTERNS 15  /* uint16 [inf 16 + lrn 16][64] pattern history rings */
+#define HTM_ST_TM_UPDATES 16   /* htm_tm_update [upd_capacity] */
+size_t htm_state_bytes(const htm_engine* eng, int32_t region);
+int htm_export_state(htm_engine* eng, int32_t region, int32_t stream_begin, int32_t n,
+                     void* h_dst, size_t bytes);
+int htm_import_state(htm_engine* eng, int32_t region, int32_t stream_begin, int32_t n,
+                     const void* h_src, size_t bytes);
+
+/* Per-stream TM bookkeeping (HTM_ST_TM_HEADER layout). */
+typedef struct {
+    uint32_t lrn_iter, iter;
+    int32_t pam_counter, learned_seq_length, reset_called, have_avg_density;
+    double avg_input_density, avg_learned_seq_length;
+    uint32_t rng_state[31];
+    int32_t rng_f, rng_r;
+    uint32_t seg_hwm, seg_live;
+    int32_t n_inf_pat, n_lrn_pat;
+    uint16_t inf_pat_len[16];
+    uint16_t lrn_pat_len[16];
+    int32_t n_upd;
+    uint32_t error;          /* bit 0 seg pool full, bit 1 update queue full */
+    uint32_t stat_inf_phase2, stat_inf_backtrack, stat_lrn_phase2, stat_lrn_backtrack;
+    uint16_t inf_pat_head, lrn_pat_head; /* ring-buffer heads of the histories */
+    uint32_t pad;
+} htm_tm_header;
+
+/* A queued segment update (BacktrackingTM segmentUpdates entry). */
+typedef struct {
+    uint32_t slot;           /* segment slot */
+    uint16_t col;
+    uint8_t cell;            /* cell index within the column */
+    uint8_t n_new;           /* new synapse sources */
+    uint32_t active_mask;    /* existing synapse positions to reinforce */
+    uint32_t date;           /* lrn_iter when queued */
+    uint16_t new_src[32];
+} htm_tm_update;
+
+/* TM reset (BacktrackingTM.reset) of every stream. */
+int htm_reset_tm(htm_engine* eng, void* stream);
+
+/* Save / load the whole engine (config + every region) to one file. */
+int htm_save(htm_engine* eng, const char* path);
+int htm_load(const char* path, int32_t device, htm_engine** out);
+
+/* Replicate stream `src` into every stream of the engine (config-2 setup:
+ * every stream starts from the same trained Model-1 state). */
+int htm_replicate_stream(htm_engine* eng, int32_t src, void* stream);
+
+/* Engine introspection */
+int32_t htm_n_streams(const htm_engine* eng);
+int htm_get_config(const htm_engine* eng, htm_config* out);
+/* Bytes of device memory held by the engine. */
+size_t htm_device_bytes(const htm_engine* eng);
+/* 1 when the frozen-TM forward index (used while TM learning is off) is
+ * current. */
+int32_t htm_frozen_index_valid(const htm_engine* eng);
+
+const char* htm_last_error(void);
+int32_t htm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,242 @@
+"""ctypes wrapper around the C oracle (oracle/htm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker.  The product (the HIP engine in
+real-time-anomaly-prediction-in-distributed-systems_amd/) never imports it.
+
+PARITY UNPINNED w.r.t. NuPIC (see htm_oracle.h and DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [
+        ("n_fields", ctypes.c_int32), ("enc_n", ctypes.c_int32), ("enc_w", ctypes.c_int32),
+        ("enc_minval", ctypes.c_double), ("enc_maxval", ctypes.c_double), ("enc_clip", ctypes.c_int32),
+        ("sp_columns", ctypes.c_int32), ("sp_num_active", ctypes.c_int32),
+        ("sp_potential_pct", ctypes.c_float), ("sp_perm_connected", ctypes.c_float),
+        ("sp_perm_active_inc", ctypes.c_float), ("sp_perm_inactive_dec", ctypes.c_float),
+        ("sp_min_pct_overlap_dc", ctypes.c_float), ("sp_duty_cycle_period", ctypes.c_int32),
+        ("sp_boost_strength", ctypes.c_float), ("sp_stimulus_threshold", ctypes.c_int32),
+        ("sp_update_period", ctypes.c_int32), ("sp_seed", ctypes.c_uint64),
+        ("tm_cells_per_col", ctypes.c_int32), ("tm_new_syn_count", ctypes.c_int32),
+        ("tm_max_syn_per_seg", ctypes.c_int32), ("tm_max_segs_per_cell", ctypes.c_int32),
+        ("tm_initial_perm", ctypes.c_float), ("tm_connected_perm", ctypes.c_float),
+        ("tm_perm_inc", ctypes.c_float), ("tm_perm_dec", ctypes.c_float), ("tm_perm_max", ctypes.c_float),
+        ("tm_min_threshold", ctypes.c_int32), ("tm_activation_threshold", ctypes.c_int32),
+        ("tm_pam_length", ctypes.c_int32), ("tm_max_inf_backtrack", ctypes.c_int32),
+        ("tm_max_lrn_backtrack", ctypes.c_int32), ("tm_max_seq_length", ctypes.c_int32),
+        ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile liboracle.so from the C sources (gcc; no HIP)."""
+    src = os.path.join(HERE, "htm_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        vp = ctypes.c_void_p
+        L.orc_default_params.argtypes = [P(OrcParams)]
+        L.orc_create.argtypes = [P(OrcParams)]
+        L.orc_create.restype = vp
+        L.orc_clone.argtypes = [vp]
+        L.orc_clone.restype = vp
+        L.orc_free.argtypes = [vp]
+        L.orc_step.argtypes = [vp, P(ctypes.c_double), ctypes.c_int, ctypes.c_int]
+        L.orc_step.restype = ctypes.c_float
+        L.orc_step_batch.argtypes = [P(vp), ctypes.c_int, P(ctypes.c_double), ctypes.c_int, ctypes.c_int,
+                                     P(ctypes.c_float), ctypes.c_int]
+        L.orc_tm_reset.argtypes = [vp]
+        L.orc_num_inputs.argtypes = [vp]
+        L.orc_num_inputs.restype = ctypes.c_int
+        L.orc_num_cells.argtypes = [vp]
+        L.orc_num_cells.restype = ctypes.c_int
+        L.orc_encode.argtypes = [vp, P(ctypes.c_double), vp]
+        L.orc_active_columns.argtypes = [vp, vp]
+        L.orc_active_columns.restype = ctypes.c_int
+        L.orc_prev_pred_columns.argtypes = [vp, vp]
+        L.orc_prev_pred_columns.restype = ctypes.c_int
+        L.orc_tm_states.argtypes = [vp, vp, vp, vp, vp]
+        L.orc_col_confidence.argtypes = [vp, vp]
+        L.orc_cell_confidence.argtypes = [vp, vp]
+        L.orc_tm_scalars.argtypes = [vp, vp]
+        L.orc_tm_avg_input_density.argtypes = [vp]
+        L.orc_tm_avg_input_density.restype = ctypes.c_double
+        L.orc_tm_stats.argtypes = [vp, vp]
+        L.orc_tm_segments.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int]
+        L.orc_tm_segments.restype = ctypes.c_int
+        L.orc_sp_state.argtypes = [vp] * 9
+        L.orc_sp_overlaps.argtypes = [vp, vp]
+        L.orc_rng_stream.argtypes = [ctypes.c_uint64, ctypes.c_int, vp]
+        L.orc_rng_real64.argtypes = [ctypes.c_uint64, ctypes.c_int, vp]
+        L.orc_tm_rng_state.argtypes = [vp, vp]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def default_params(**overrides) -> OrcParams:
+    p = OrcParams()
+    lib().orc_default_params(ctypes.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+class OracleModel:
+    """One Model-1 stream (encoder -> SP -> TM -> raw anomaly) on the CPU."""
+
+    def __init__(self, params: OrcParams | None = None, _handle=None, **overrides):
+        self.params = params if params is not None else default_params(**overrides)
+        if _handle is not None:
+            self.h = _handle
+        else:
+            self.h = lib().orc_create(ctypes.byref(self.params))
+            if not self.h:
+                raise ValueError("orc_create rejected the parameters")
+        self.n_inputs = lib().orc_num_inputs(self.h)
+        self.n_cells = lib().orc_num_cells(self.h)
+        self.n_cols = self.params.sp_columns
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib is not None:
+            _lib.orc_free(h)
+            self.h = None
+
+    def clone(self) -> "OracleModel":
+        return OracleModel(self.params, _handle=lib().orc_clone(self.h))
+
+    def step(self, values, sp_learn: bool, tm_learn: bool) -> np.float32:
+        v = np.ascontiguousarray(np.atleast_1d(np.asarray(values, dtype=np.float64)))
+        return np.float32(lib().orc_step(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                         int(sp_learn), int(tm_learn)))
+
+    def tm_reset(self):
+        lib().orc_tm_reset(self.h)
+
+    def encode(self, values) -> np.ndarray:
+        v = np.ascontiguousarray(np.atleast_1d(np.asarray(values, dtype=np.float64)))
+        out = np.zeros(self.n_inputs, np.uint8)
+        lib().orc_encode(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), _ptr(out))
+        return out
+
+    def active_columns(self) -> np.ndarray:
+        out = np.zeros(self.n_cols, np.int32)
+        n = lib().orc_active_columns(self.h, _ptr(out))
+        return out[:n].copy()
+
+    def prev_pred_columns(self) -> np.ndarray:
+        out = np.zeros(self.n_cols, np.int32)
+        n = lib().orc_prev_pred_columns(self.h, _ptr(out))
+        return out[:n].copy()
+
+    def tm_states(self):
+        a = [np.zeros(self.n_cells, np.uint8) for _ in range(4)]
+        lib().orc_tm_states(self.h, *[_ptr(x) for x in a])
+        return dict(inf_active=a[0], inf_pred=a[1], lrn_active=a[2], lrn_pred=a[3])
+
+    def col_confidence(self) -> np.ndarray:
+        out = np.zeros(self.n_cols, np.float32)
+        lib().orc_col_confidence(self.h, _ptr(out))
+        return out
+
+    def cell_confidence(self) -> np.ndarray:
+        out = np.zeros(self.n_cells, np.float32)
+        lib().orc_cell_confidence(self.h, _ptr(out))
+        return out
+
+    def tm_scalars(self) -> dict:
+        out = np.zeros(9, np.int64)
+        lib().orc_tm_scalars(self.h, _ptr(out))
+        keys = ["lrn_iter", "iter", "pam_counter", "learned_seq_length", "n_prev_inf",
+                "n_prev_lrn", "n_updates", "n_segments", "n_synapses"]
+        d = {k: int(v) for k, v in zip(keys, out)}
+        d["avg_input_density"] = lib().orc_tm_avg_input_density(self.h)
+        return d
+
+    def tm_stats(self) -> dict:
+        out = np.zeros(4, np.int64)
+        lib().orc_tm_stats(self.h, _ptr(out))
+        return dict(inf_phase2=int(out[0]), inf_backtracks=int(out[1]), lrn_phase2=int(out[2]),
+                    lrn_backtracks=int(out[3]))
+
+    def tm_segments(self, max_syn: int = 64) -> dict:
+        n = lib().orc_tm_segments(self.h, None, None, None, None, max_syn)
+        info = np.zeros((n, 5), np.int32)
+        dc = np.zeros(n, np.float32)
+        src = np.zeros((n, max_syn), np.int32)
+        perm = np.zeros((n, max_syn), np.float32)
+        if n:
+            lib().orc_tm_segments(self.h, _ptr(info), _ptr(dc), _ptr(src), _ptr(perm), max_syn)
+        return dict(cell=info[:, 0], is_seq=info[:, 1], pos_act=info[:, 2], last_dc_iter=info[:, 3],
+                    nsyn=info[:, 4], last_dc=dc, src=src, perm=perm)
+
+    def sp_state(self) -> dict:
+        C, I = self.n_cols, self.n_inputs
+        perm = np.zeros((C, I), np.float32)
+        pot = np.zeros((C, I), np.uint8)
+        conn = np.zeros((C, I), np.uint8)
+        odc, adc, mdc, boost = (np.zeros(C, np.float32) for _ in range(4))
+        it2 = np.zeros(2, np.int64)
+        lib().orc_sp_state(self.h, *[_ptr(x) for x in (perm, pot, conn, odc, adc, mdc, boost, it2)])
+        return dict(perm=perm, potential=pot, connected=conn, overlap_dc=odc, active_dc=adc,
+                    min_overlap_dc=mdc, boost=boost, iter=int(it2[0]), iter_learn=int(it2[1]))
+
+    def sp_overlaps(self) -> np.ndarray:
+        out = np.zeros(self.n_cols, np.int32)
+        lib().orc_sp_overlaps(self.h, _ptr(out))
+        return out
+
+    def tm_rng_state(self) -> np.ndarray:
+        out = np.zeros(33, np.uint32)
+        lib().orc_tm_rng_state(self.h, _ptr(out))
+        return out
+
+
+def step_batch(models, values: np.ndarray, sp_learn: bool, tm_learn: bool, n_threads: int = 0) -> np.ndarray:
+    """Step many oracle streams (OpenMP across streams)."""
+    n = len(models)
+    arr = (ctypes.c_void_p * n)(*[m.h for m in models])
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    out = np.zeros(n, np.float32)
+    lib().orc_step_batch(arr, n, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(sp_learn),
+                         int(tm_learn), out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(n_threads))
+    return out
+
+
+def rng_stream(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.uint32)
+    lib().orc_rng_stream(seed, n, _ptr(out))
+    return out
+
+
+def rng_real64(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.float64)
+    lib().orc_rng_real64(seed, n, _ptr(out))
+    return out

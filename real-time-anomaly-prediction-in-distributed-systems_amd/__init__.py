@@ -1,0 +1,10 @@
+"""MI355X-native batched HTM engine (encoder -> SP -> BacktrackingTM -> anomaly).
+
+Import through the repo-root helper `_pkg.load()` (the package directory name
+is not a Python identifier); it registers this package as `rtap_amd`.
+"""
+from . import _lib
+from ._lib import HtmConfig, HtmError, build, default_config
+from .engine import HTMEngine
+
+__all__ = ["HTMEngine", "HtmConfig", "HtmError", "build", "default_config", "_lib"]

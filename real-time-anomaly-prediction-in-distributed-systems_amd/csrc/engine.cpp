@@ -1,0 +1,685 @@
+// engine.cpp -- host side of the C ABI (include/htm_amd.h).
+//
+// Owns the device memory of all streams (one hipMalloc per buffer, sized
+// from the config), derives the immutable kernel constants, and sequences
+// the per-step launches: SP kernel then TM kernel on the caller's stream.
+// The TM kernel variant follows the learning flags: learning on -> pool
+// scans; learning off -> frozen forward index (built on the first frozen
+// step after learning, one count/scan/fill pass per stream).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "htm_dev.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(x)                                                                          \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) return fail(HTM_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct Region {
+    void* base;
+    size_t per_stream;
+};
+
+struct htm_engine {
+    htm_config cfg;
+    DevCfg dc;
+    int32_t n;
+    int32_t device;
+    SpBufs sp;
+    TmBufs tm;
+    std::vector<void*> allocs;
+    size_t bytes = 0;
+    int32_t sp_learn = 1, tm_learn = 1;
+    int32_t use_frozen = 1;
+    int32_t keep_prev = 0;
+    int32_t keep_overlaps = 0;
+    bool fx_valid = false;
+    size_t fx_cap = 0;
+    uint64_t* d_counts = nullptr;
+    Region regions[17];
+};
+
+extern "C" {
+
+void htm_default_config(htm_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->n_fields = 1;
+    c->enc_n = 500;
+    c->enc_w = 21;
+    c->enc_minval = 0.0;
+    c->enc_maxval = 100.0;
+    c->enc_clip = 1;
+    c->sp_columns = 2048;
+    c->sp_num_active = 40;
+    c->sp_potential_pct = 0.8f;
+    c->sp_perm_connected = 0.1f;
+    c->sp_perm_active_inc = 0.0001f;
+    c->sp_perm_inactive_dec = 0.0005f;
+    c->sp_min_pct_overlap_dc = 0.001f;
+    c->sp_duty_cycle_period = 1000;
+    c->sp_boost_strength = 0.0f;
+    c->sp_stimulus_threshold = 0;
+    c->sp_update_period = 50;
+    c->sp_seed = 2045;
+    c->tm_cells_per_col = 12;
+    c->tm_new_syn_count = 20;
+    c->tm_max_syn_per_seg = 32;
+    c->tm_max_segs_per_cell = 128;
+    c->tm_initial_perm = 0.21f;
+    c->tm_connected_perm = 0.5f;
+    c->tm_perm_inc = 0.1f;
+    c->tm_perm_dec = 0.1f;
+    c->tm_perm_max = 1.0f;
+    c->tm_min_threshold = 9;
+    c->tm_activation_threshold = 12;
+    c->tm_pam_length = 3;
+    c->tm_max_inf_backtrack = 10;
+    c->tm_max_lrn_backtrack = 5;
+    c->tm_max_seq_length = 32;
+    c->tm_seg_update_valid_duration = 5;
+    c->tm_seed = 2045;
+    c->seg_capacity = 1 << 17;
+    c->upd_capacity = 2048;
+    c->seed_stride = 0;
+}
+
+}  // extern "C"
+
+static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) {
+    if (c.n_fields < 1 || c.n_fields > 4) return fail(HTM_E_INVALID, "n_fields must be 1..4");
+    if (c.enc_w < 1 || c.enc_w >= c.enc_n || c.enc_n * c.n_fields > 2048)
+        return fail(HTM_E_INVALID, "encoder n/w out of range");
+    if (c.n_fields * c.enc_w >= 128) return fail(HTM_E_INVALID, "n_fields*w must be < 128");
+    if (c.sp_columns < 64 || c.sp_columns % 64 != 0 || c.sp_columns > 4096)
+        return fail(HTM_E_INVALID, "sp_columns must be a multiple of 64 in [64, 4096]");
+    if (c.sp_num_active < 1 || c.sp_num_active > HTM_MAXACT) return fail(HTM_E_INVALID, "sp_num_active must be 1..64");
+    if (c.sp_boost_strength != 0.0f) return fail(HTM_E_INVALID, "only boostStrength 0 is supported");
+    if (c.sp_stimulus_threshold < 0 || c.sp_stimulus_threshold > 127) return fail(HTM_E_INVALID, "stimulus threshold");
+    if (c.tm_cells_per_col < 2 || c.tm_cells_per_col > HTM_MAXK) return fail(HTM_E_INVALID, "cells_per_col must be 2..32");
+    if ((int64_t)c.sp_columns * c.tm_cells_per_col > 65536) return fail(HTM_E_INVALID, "columns*cells must be <= 65536");
+    if (c.tm_max_syn_per_seg < 1 || c.tm_max_syn_per_seg > HTM_MAXSYN) return fail(HTM_E_INVALID, "max_syn_per_seg 1..32");
+    if (c.tm_new_syn_count < 1 || c.tm_new_syn_count > c.tm_max_syn_per_seg)
+        return fail(HTM_E_INVALID, "new_syn_count must be 1..max_syn_per_seg");
+    if (c.tm_max_segs_per_cell < 1 || c.tm_max_segs_per_cell > 255) return fail(HTM_E_INVALID, "max_segs_per_cell 1..255");
+    if (c.tm_max_inf_backtrack < 0 || c.tm_max_inf_backtrack > HTM_MAXPAT - 1 || c.tm_max_lrn_backtrack < 0 ||
+        c.tm_max_lrn_backtrack > HTM_MAXPAT - 1)
+        return fail(HTM_E_INVALID, "backtrack depth must be 0..15");
+    if (c.tm_pam_length < 1) return fail(HTM_E_INVALID, "pamLength must be > 0");
+    if (c.seg_capacity < 64 || c.seg_capacity > (1 << 27)) return fail(HTM_E_INVALID, "seg_capacity");
+    if (c.upd_capacity < 1 || c.upd_capacity > 65535) return fail(HTM_E_INVALID, "upd_capacity");
+    std::memset(&d, 0, sizeof(d));
+    d.n_fields = c.n_fields;
+    d.enc_n = c.enc_n;
+    d.enc_w = c.enc_w;
+    d.enc_clip = c.enc_clip;
+    d.enc_min = c.enc_minval;
+    d.enc_max = c.enc_maxval;
+    d.enc_resolution = (c.enc_maxval - c.enc_minval) / (double)(c.enc_n - c.enc_w);
+    d.enc_halfwidth = (c.enc_w - 1) / 2;
+    d.nin = c.n_fields * c.enc_n;
+    d.nin_pad = (int32_t)round_up((size_t)d.nin, 32);
+    d.ncol = c.sp_columns;
+    d.nw = c.sp_columns / 32;
+    // mapPotential_: WrappingNeighborhood(radius = inputWidth) covers all inputs
+    d.n_potential = (int32_t)roundf((float)d.nin * c.sp_potential_pct);
+    // inhibitColumns_: inhibitionRadius = max(columnDimensions) (global)
+    uint32_t area = (uint32_t)powf((float)(2 * c.sp_columns + 1), 1.0f);
+    if (area > (uint32_t)c.sp_columns) area = (uint32_t)c.sp_columns;
+    float density = (float)c.sp_num_active / (float)area;
+    if (density > 0.5f) density = 0.5f;
+    d.num_desired = (int32_t)(uint32_t)(density * (float)c.sp_columns);
+    if (d.num_desired > HTM_MAXACT) return fail(HTM_E_INVALID, "too many winners");
+    d.stim_thr = c.sp_stimulus_threshold;
+    d.dc_period = c.sp_duty_cycle_period;
+    d.update_period = c.sp_update_period;
+    d.sp_conn = c.sp_perm_connected;
+    d.sp_conn_thr = c.sp_perm_connected - 0.000001f;
+    d.sp_inc = c.sp_perm_active_inc;
+    d.sp_dec = c.sp_perm_inactive_dec;
+    d.sp_trim = (float)((double)c.sp_perm_active_inc / 2.0);
+    d.sp_below_inc = (float)((double)c.sp_perm_connected / 10.0);
+    d.sp_min_pct_odc = c.sp_min_pct_overlap_dc;
+    d.K = c.tm_cells_per_col;
+    d.ncells = c.sp_columns * c.tm_cells_per_col;
+    d.cw = d.ncells / 32;
+    d.kmagic = (uint32_t)((4294967296ull + (uint64_t)d.K - 1) / (uint64_t)d.K);
+    d.new_syn = c.tm_new_syn_count;
+    d.max_syn = c.tm_max_syn_per_seg;
+    d.max_segs_per_cell = c.tm_max_segs_per_cell;
+    d.init_perm = c.tm_initial_perm;
+    d.tm_conn = c.tm_connected_perm;
+    d.tm_inc = c.tm_perm_inc;
+    d.tm_dec = c.tm_perm_dec;
+    d.tm_max = c.tm_perm_max;
+    d.min_thr = c.tm_min_threshold;
+    d.act_thr = c.tm_activation_threshold;
+    d.pam_len = c.tm_pam_length;
+    d.max_inf_bt = c.tm_max_inf_backtrack;
+    d.max_lrn_bt = c.tm_max_lrn_backtrack;
+    d.max_seq_len = c.tm_max_seq_length;
+    d.upd_valid = c.tm_seg_update_valid_duration;
+    d.seg_cap = c.seg_capacity;
+    d.upd_cap = c.upd_capacity;
+    d.seg_reserve = (c.tm_max_lrn_backtrack + 2) * c.sp_num_active;
+    if (d.seg_reserve >= d.seg_cap) return fail(HTM_E_INVALID, "seg_capacity too small for one learning step");
+    d.n_streams = n;
+    // frozen-inference counter window: the union region holds the u8
+    // counters (fx_win bytes) plus the active-cell list (4 KiB); fill the
+    // LDS budget so that two workgroups fit one CU
+    d.fx_win = 0;
+    d.fx_nwin = 1;
+    d.fx_win = 1024;  // provisional, to measure the rest of the layout
+    size_t off_u = tm_step_lds_bytes(d, 0, 1) - (size_t)(1024 / 4 + 1024) * 4;
+    size_t fin = ((size_t)d.ncol + (size_t)(d.ncol + 1) / 2 + (size_t)d.ncol + 1) * 4;
+    size_t win = lds_budget > off_u + 4096 ? lds_budget - off_u - 4096 : 0;
+    if (win < fin) win = fin;  // the union is at least the finish arrays anyway
+    win = (win / 1024) * 1024;
+    if (win < 4096) win = 4096;
+    size_t capr = round_up((size_t)d.seg_cap, 1024);
+    if (win > capr) win = capr;
+    d.fx_win = (int32_t)win;
+    d.fx_nwin = (int32_t)((d.seg_cap + d.fx_win - 1) / d.fx_win);
+    return HTM_OK;
+}
+
+static int dalloc(htm_engine* e, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t err = hipMalloc(p, bytes);
+    if (err != hipSuccess) return fail(HTM_E_HIP, "hipMalloc(%zu): %s", bytes, hipGetErrorString(err));
+    err = hipMemset(*p, 0, bytes);
+    if (err != hipSuccess) return fail(HTM_E_HIP, "hipMemset: %s", hipGetErrorString(err));
+    e->allocs.push_back(*p);
+    e->bytes += bytes;
+    return HTM_OK;
+}
+
+#define ALLOC(field, T, count)                                                     \
+    do {                                                                           \
+        void* p_ = nullptr;                                                        \
+        int r_ = dalloc(e, &p_, (size_t)(count) * sizeof(T));                      \
+        if (r_) return r_;                                                         \
+        field = reinterpret_cast<T*>(p_);                                          \
+    } while (0)
+
+static int allocate(htm_engine* e) {
+    const DevCfg& d = e->dc;
+    const size_t S = (size_t)e->n;
+    const size_t cap = (size_t)d.seg_cap;
+    ALLOC(e->sp.connT, uint32_t, S * d.nin_pad * d.nw);
+    ALLOC(e->sp.potmask, uint32_t, S * d.ncol * (d.nin_pad / 32));
+    ALLOC(e->sp.perm, float, S * d.ncol * d.n_potential);
+    ALLOC(e->sp.duty, float, S * 2 * d.ncol);
+    ALLOC(e->sp.scalars, uint32_t, S * 4);
+    ALLOC(e->sp.act, uint16_t, S * HTM_MAXACT);
+    ALLOC(e->sp.nact, uint32_t, S);
+    ALLOC(e->sp.overlaps, int32_t, S * d.ncol);
+    ALLOC(e->sp.seeds, uint64_t, S);
+    ALLOC(e->tm.hdr, htm_tm_header, S);
+    ALLOC(e->tm.bm, uint32_t, S * 4 * d.cw);
+    ALLOC(e->tm.colconf, float, S * d.ncol);
+    ALLOC(e->tm.pat, uint16_t, S * 2 * HTM_MAXPAT * HTM_MAXACT);
+    ALLOC(e->tm.seg_meta, uint32_t, S * cap);
+    ALLOC(e->tm.seg_src, uint16_t, S * cap * HTM_MAXSYN);
+    ALLOC(e->tm.seg_perm, float, S * cap * HTM_MAXSYN);
+    ALLOC(e->tm.seg_conn, uint32_t, S * cap);
+    ALLOC(e->tm.seg_duty, uint32_t, S * cap * 3);
+    ALLOC(e->tm.cell_nseg, uint8_t, S * d.ncells);
+    ALLOC(e->tm.upd, htm_tm_update, S * d.upd_cap);
+    ALLOC(e->tm.scr_bm, uint32_t, S * 5 * d.cw);
+    ALLOC(e->tm.scr_conf, float, S * d.ncol);
+    ALLOC(e->tm.scr_q, uint32_t, S * cap);
+    ALLOC(e->tm.scr_q2, uint32_t, S * cap);
+    ALLOC(e->tm.scr_cur, uint32_t, S * (size_t)d.ncells * d.fx_nwin);
+    ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
+    ALLOC(e->tm.fx_base, uint64_t, S);
+    ALLOC(e->tm.fx_off, uint32_t, S * ((size_t)d.ncells * d.fx_nwin + 1));
+    ALLOC(e->d_counts, uint64_t, S);
+    e->tm.fx_ent = nullptr;
+    // region table for export / import / save / load / replicate
+    Region* r = e->regions;
+    for (int i = 0; i < 17; i++) r[i] = Region{nullptr, 0};
+    r[HTM_ST_SP_CONNT] = {e->sp.connT, (size_t)d.nin_pad * d.nw * 4};
+    r[HTM_ST_SP_POTMASK] = {e->sp.potmask, (size_t)d.ncol * (d.nin_pad / 32) * 4};
+    r[HTM_ST_SP_PERM] = {e->sp.perm, (size_t)d.ncol * d.n_potential * 4};
+    r[HTM_ST_SP_DUTY] = {e->sp.duty, (size_t)2 * d.ncol * 4};
+    r[HTM_ST_SP_SCALARS] = {e->sp.scalars, 16};
+    r[HTM_ST_TM_HEADER] = {e->tm.hdr, sizeof(htm_tm_header)};
+    r[HTM_ST_TM_BITMAPS] = {e->tm.bm, (size_t)4 * d.cw * 4};
+    r[HTM_ST_TM_COLCONF] = {e->tm.colconf, (size_t)d.ncol * 4};
+    r[HTM_ST_TM_SEG_META] = {e->tm.seg_meta, cap * 4};
+    r[HTM_ST_TM_SEG_SRC] = {e->tm.seg_src, cap * HTM_MAXSYN * 2};
+    r[HTM_ST_TM_SEG_PERM] = {e->tm.seg_perm, cap * HTM_MAXSYN * 4};
+    r[HTM_ST_TM_SEG_CONN] = {e->tm.seg_conn, cap * 4};
+    r[HTM_ST_TM_SEG_DUTY] = {e->tm.seg_duty, cap * 12};
+    r[HTM_ST_TM_CELL_NSEG] = {e->tm.cell_nseg, (size_t)d.ncells};
+    r[HTM_ST_TM_PATTERNS] = {e->tm.pat, (size_t)2 * HTM_MAXPAT * HTM_MAXACT * 2};
+    r[HTM_ST_TM_UPDATES] = {e->tm.upd, (size_t)d.upd_cap * sizeof(htm_tm_update)};
+    return HTM_OK;
+}
+
+static int query_lds_optin() {
+    int dev = 0, v = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || v <= 0) {
+        (void)hipGetLastError();
+        v = 65536;
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+    }
+    return v;
+}
+
+static int check_lds(const DevCfg& d) {
+    int maxlds = query_lds_optin();
+    for (int learn = 0; learn < 2; learn++)
+        for (int fz = 0; fz < 2; fz++) {
+            if (learn && fz) continue;
+            size_t b = tm_step_lds_bytes(d, learn, fz);
+            if (b > (size_t)maxlds) return fail(HTM_E_INVALID, "TM kernel needs %zu B LDS > %d", b, maxlds);
+        }
+    return HTM_OK;
+}
+
+static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out) {
+    if (!cfg || !out || n_streams < 1) return fail(HTM_E_INVALID, "bad arguments");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    htm_engine* e = new htm_engine();
+    e->cfg = *cfg;
+    e->n = n_streams;
+    e->device = device;
+    int optin = query_lds_optin();
+    size_t budget = optin >= 78 * 1024 ? (size_t)76 * 1024 : (size_t)optin - 2048;
+    int r = derive(*cfg, n_streams, budget, e->dc);
+    if (!r) r = check_lds(e->dc);
+    if (!r) r = allocate(e);
+    if (!r && tm_configure_lds(e->dc) && tm_step_lds_bytes(e->dc, 0, 1) > 65536)
+        r = fail(HTM_E_HIP, "cannot raise the dynamic LDS limit to %zu B", tm_step_lds_bytes(e->dc, 0, 1));
+    if (r) {
+        for (void* p : e->allocs) hipFree(p);
+        delete e;
+        return r;
+    }
+    *out = e;
+    return HTM_OK;
+}
+
+extern "C" {
+
+int htm_create(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out) {
+    int r = create_uninit(cfg, n_streams, device, out);
+    if (r) return r;
+    htm_engine* e = *out;
+    std::vector<uint64_t> seeds((size_t)n_streams);
+    for (int s = 0; s < n_streams; s++) seeds[s] = cfg->sp_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
+    hipError_t err = hipMemcpy(e->sp.seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice);
+    if (err != hipSuccess) return fail(HTM_E_HIP, "seed upload: %s", hipGetErrorString(err));
+    if (launch_sp_init(e->dc, e->sp, n_streams, 0)) return fail(HTM_E_HIP, "sp_init launch failed");
+    for (int s = 0; s < n_streams; s++) seeds[s] = cfg->tm_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
+    uint64_t* dseeds = nullptr;
+    HIP_TRY(hipMalloc(&dseeds, seeds.size() * 8));
+    HIP_TRY(hipMemcpy(dseeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
+    if (launch_tm_init(e->dc, e->tm, dseeds, n_streams, 0)) return fail(HTM_E_HIP, "tm_init launch failed");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree(dseeds));
+    return HTM_OK;
+}
+
+int htm_destroy(htm_engine* e) {
+    if (!e) return HTM_OK;
+    hipSetDevice(e->device);
+    hipDeviceSynchronize();
+    for (void* p : e->allocs) hipFree(p);
+    if (e->tm.fx_ent) hipFree(e->tm.fx_ent);
+    delete e;
+    return HTM_OK;
+}
+
+int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
+    if (!e) return fail(HTM_E_INVALID, "null engine");
+    e->sp_learn = sp_learn ? 1 : 0;
+    if (tm_learn && !e->tm_learn) e->fx_valid = false;
+    e->tm_learn = tm_learn ? 1 : 0;
+    return HTM_OK;
+}
+
+int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
+    if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (opt == HTM_OPT_FROZEN_INDEX) e->use_frozen = value ? 1 : 0;
+    else if (opt == HTM_OPT_KEEP_PREV) e->keep_prev = value ? 1 : 0;
+    else if (opt == HTM_OPT_KEEP_OVERLAPS) e->keep_overlaps = value ? 1 : 0;
+    else return fail(HTM_E_INVALID, "unknown option %d", opt);
+    return HTM_OK;
+}
+
+}  // extern "C"
+
+static int build_fx(htm_engine* e, hipStream_t st) {
+    const DevCfg& d = e->dc;
+    if (launch_tm_fx_count(d, e->tm, e->d_counts, e->n, st)) return fail(HTM_E_HIP, "fx count launch");
+    std::vector<uint64_t> counts((size_t)e->n);
+    HIP_TRY(hipMemcpyAsync(counts.data(), e->d_counts, counts.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint64_t> base((size_t)e->n);
+    uint64_t tot = 0;
+    for (int s = 0; s < e->n; s++) {
+        base[s] = tot;
+        tot += counts[s];
+    }
+    if (tot == 0) tot = 1;
+    if (tot > e->fx_cap) {
+        if (e->tm.fx_ent) HIP_TRY(hipFree(e->tm.fx_ent));
+        e->tm.fx_ent = nullptr;
+        size_t cap = (size_t)(tot + tot / 8 + 1024);
+        HIP_TRY(hipMalloc(&e->tm.fx_ent, cap * 4));
+        e->fx_cap = cap;
+    }
+    HIP_TRY(hipMemcpyAsync(e->tm.fx_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
+    if (launch_tm_fx_fill(d, e->tm, e->n, st)) return fail(HTM_E_HIP, "fx fill launch");
+    HIP_TRY(hipStreamSynchronize(st));
+    e->fx_valid = true;
+    return HTM_OK;
+}
+
+extern "C" {
+
+int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
+    if (!e || !d_values || !d_scores) return fail(HTM_E_INVALID, "bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    if (launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st)) return fail(HTM_E_HIP, "sp_step launch");
+    int frozen = 0;
+    if (e->tm_learn) {
+        e->fx_valid = false;
+    } else if (e->use_frozen) {
+        if (!e->fx_valid) {
+            int r = build_fx(e, st);
+            if (r) return r;
+        }
+        frozen = 1;
+    }
+    if (e->keep_prev) {
+        // prevPredictedColumns (nonzero colConfidence before compute)
+        if (launch_prev_pred(e->dc, e->tm, e->n, st)) return fail(HTM_E_HIP, "prev_pred launch");
+    }
+    if (launch_tm_step(e->dc, e->tm, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
+        return fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
+    return HTM_OK;
+}
+
+int htm_run(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, void* stream) {
+    if (!e) return fail(HTM_E_INVALID, "null engine");
+    const size_t stride = (size_t)e->n * e->cfg.n_fields;
+    for (int32_t k = 0; k < n_steps; k++) {
+        int r = htm_step(e, d_values + (size_t)k * stride, d_scores + (size_t)k * e->n, stream);
+        if (r) return r;
+    }
+    return HTM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// outputs
+__global__ void out_kernel(DevCfg c, SpBufs sp, TmBufs tm, int which, uint8_t* dst) {
+    const int s = blockIdx.x;
+    if (which == HTM_OUT_ACTIVE_COLUMNS) {
+        uint8_t* o = dst + (size_t)s * c.ncol;
+        for (int i = threadIdx.x; i < c.ncol; i += blockDim.x) o[i] = 0;
+        __syncthreads();
+        uint32_t n = sp.nact[s];
+        for (uint32_t i = threadIdx.x; i < n && i < HTM_MAXACT; i += blockDim.x) o[sp.act[(size_t)s * HTM_MAXACT + i]] = 1;
+    } else if (which == HTM_OUT_PREV_PRED_COLS) {
+        uint8_t* o = dst + (size_t)s * c.ncol;
+        for (int i = threadIdx.x; i < c.ncol; i += blockDim.x) o[i] = tm.prev_pred[(size_t)s * c.ncol + i];
+    } else if (which == HTM_OUT_TM_OUTPUT) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(dst) + (size_t)s * c.cw;
+        const uint32_t* bm = tm.bm + (size_t)s * 4 * c.cw;
+        for (int i = threadIdx.x; i < c.cw; i += blockDim.x) o[i] = bm[i] | bm[c.cw + i];
+    }
+}
+
+__global__ void prev_pred_kernel(DevCfg c, TmBufs tm) {
+    const int s = blockIdx.x;
+    for (int i = threadIdx.x; i < c.ncol; i += blockDim.x)
+        tm.prev_pred[(size_t)s * c.ncol + i] = tm.colconf[(size_t)s * c.ncol + i] != 0.0f ? 1 : 0;
+}
+
+int launch_prev_pred(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+    hipLaunchKernelGGL(prev_pred_kernel, dim3(n), dim3(256), 0, st, c, b);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" {
+
+size_t htm_output_bytes(const htm_engine* e, int32_t which) {
+    if (!e) return 0;
+    const DevCfg& d = e->dc;
+    switch (which) {
+        case HTM_OUT_ACTIVE_COLUMNS:
+        case HTM_OUT_PREV_PRED_COLS: return (size_t)d.ncol;
+        case HTM_OUT_INF_ACTIVE:
+        case HTM_OUT_INF_PREDICTED:
+        case HTM_OUT_LRN_ACTIVE:
+        case HTM_OUT_LRN_PREDICTED:
+        case HTM_OUT_TM_OUTPUT: return (size_t)d.cw * 4;
+        case HTM_OUT_COL_CONFIDENCE: return (size_t)d.ncol * 4;
+        case HTM_OUT_SP_OVERLAPS: return (size_t)d.ncol * 4;
+        default: return 0;
+    }
+}
+
+int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void* stream) {
+    if (!e || !d_dst) return fail(HTM_E_INVALID, "bad arguments");
+    size_t per = htm_output_bytes(e, which);
+    if (!per) return fail(HTM_E_INVALID, "unknown output %d", which);
+    if (bytes < per * e->n) return fail(HTM_E_INVALID, "output buffer too small (%zu < %zu)", bytes, per * e->n);
+    hipStream_t st = (hipStream_t)stream;
+    const DevCfg& d = e->dc;
+    switch (which) {
+        case HTM_OUT_ACTIVE_COLUMNS:
+        case HTM_OUT_PREV_PRED_COLS:
+        case HTM_OUT_TM_OUTPUT:
+            if (which == HTM_OUT_PREV_PRED_COLS && !e->keep_prev)
+                return fail(HTM_E_STATE, "prev-predicted columns need htm_set_option(KEEP_PREV)");
+            hipLaunchKernelGGL(out_kernel, dim3(e->n), dim3(256), 0, st, d, e->sp, e->tm, which, (uint8_t*)d_dst);
+            HIP_TRY(hipGetLastError());
+            return HTM_OK;
+        case HTM_OUT_INF_ACTIVE:
+        case HTM_OUT_INF_PREDICTED:
+        case HTM_OUT_LRN_ACTIVE:
+        case HTM_OUT_LRN_PREDICTED: {
+            int k = which - HTM_OUT_INF_ACTIVE;
+            HIP_TRY(hipMemcpy2DAsync(d_dst, per, e->tm.bm + (size_t)k * d.cw, (size_t)4 * d.cw * 4, per, e->n,
+                                     hipMemcpyDeviceToDevice, st));
+            return HTM_OK;
+        }
+        case HTM_OUT_COL_CONFIDENCE:
+            HIP_TRY(hipMemcpyAsync(d_dst, e->tm.colconf, per * e->n, hipMemcpyDeviceToDevice, st));
+            return HTM_OK;
+        case HTM_OUT_SP_OVERLAPS:
+            if (!e->keep_overlaps) return fail(HTM_E_STATE, "SP overlaps need htm_set_option(KEEP_OVERLAPS)");
+            HIP_TRY(hipMemcpyAsync(d_dst, e->sp.overlaps, per * e->n, hipMemcpyDeviceToDevice, st));
+            return HTM_OK;
+    }
+    return fail(HTM_E_INVALID, "unknown output");
+}
+
+size_t htm_state_bytes(const htm_engine* e, int32_t region) {
+    if (!e || region < 1 || region > 16) return 0;
+    return e->regions[region].per_stream;
+}
+
+int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void* h_dst, size_t bytes) {
+    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > e->n)
+        return fail(HTM_E_INVALID, "bad export arguments");
+    const Region& r = e->regions[region];
+    if (bytes < r.per_stream * n) return fail(HTM_E_INVALID, "export buffer too small");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(h_dst, (uint8_t*)r.base + r.per_stream * s0, r.per_stream * n, hipMemcpyDeviceToHost));
+    return HTM_OK;
+}
+
+int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes) {
+    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > e->n)
+        return fail(HTM_E_INVALID, "bad import arguments");
+    const Region& r = e->regions[region];
+    if (bytes < r.per_stream * n) return fail(HTM_E_INVALID, "import buffer too small");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy((uint8_t*)r.base + r.per_stream * s0, h_src, r.per_stream * n, hipMemcpyHostToDevice));
+    if (region >= HTM_ST_TM_HEADER) e->fx_valid = false;
+    return HTM_OK;
+}
+
+int htm_reset_tm(htm_engine* e, void* stream) {
+    if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (launch_tm_reset(e->dc, e->tm, e->n, (hipStream_t)stream)) return fail(HTM_E_HIP, "reset launch");
+    return HTM_OK;
+}
+
+int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
+    if (!e || src < 0 || src >= e->n) return fail(HTM_E_INVALID, "bad source stream");
+    hipStream_t st = (hipStream_t)stream;
+    for (int id = 1; id <= 16; id++) {
+        const Region& r = e->regions[id];
+        if (!r.base) continue;
+        const uint8_t* sp = (const uint8_t*)r.base + r.per_stream * src;
+        for (int s = 0; s < e->n; s++) {
+            if (s == src) continue;
+            HIP_TRY(hipMemcpyAsync((uint8_t*)r.base + r.per_stream * s, sp, r.per_stream, hipMemcpyDeviceToDevice, st));
+        }
+    }
+    // SP active list of the last step too (the TM reads it)
+    for (int s = 0; s < e->n; s++) {
+        if (s == src) continue;
+        HIP_TRY(hipMemcpyAsync(e->sp.act + (size_t)s * HTM_MAXACT, e->sp.act + (size_t)src * HTM_MAXACT,
+                               HTM_MAXACT * 2, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(e->sp.nact + s, e->sp.nact + src, 4, hipMemcpyDeviceToDevice, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    e->fx_valid = false;
+    return HTM_OK;
+}
+
+int32_t htm_n_streams(const htm_engine* e) { return e ? e->n : 0; }
+
+int htm_get_config(const htm_engine* e, htm_config* out) {
+    if (!e || !out) return fail(HTM_E_INVALID, "bad arguments");
+    *out = e->cfg;
+    return HTM_OK;
+}
+
+size_t htm_device_bytes(const htm_engine* e) { return e ? e->bytes + e->fx_cap * 4 : 0; }
+
+int32_t htm_frozen_index_valid(const htm_engine* e) { return e && e->fx_valid ? 1 : 0; }
+
+const char* htm_last_error(void) { return g_err.c_str(); }
+
+int32_t htm_abi_version(void) { return HTM_ABI_VERSION; }
+
+// Synchronise and report per-stream error flags (pool/queue overflow).
+int htm_status(htm_engine* e) {
+    if (!e) return fail(HTM_E_INVALID, "null engine");
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<htm_tm_header> h((size_t)e->n);
+    HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
+    for (int s = 0; s < e->n; s++) {
+        if (h[s].error) return fail(HTM_E_CAPACITY, "stream %d error flags 0x%x (1: segment pool full, 2: update queue full, 4: >1 learn-predicted cell, 8: learn-active list overflow)", s, h[s].error);
+    }
+    return HTM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// save / load: "HTMAMD01", abi, config, n, learning flags, then regions
+int htm_save(htm_engine* e, const char* path) {
+    if (!e || !path) return fail(HTM_E_INVALID, "bad arguments");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(HTM_E_IO, "cannot open %s", path);
+    const char magic[8] = {'H', 'T', 'M', 'A', 'M', 'D', '0', '1'};
+    int32_t abi = HTM_ABI_VERSION;
+    bool ok = std::fwrite(magic, 8, 1, f) == 1 && std::fwrite(&abi, 4, 1, f) == 1 &&
+              std::fwrite(&e->cfg, sizeof(htm_config), 1, f) == 1 && std::fwrite(&e->n, 4, 1, f) == 1 &&
+              std::fwrite(&e->sp_learn, 4, 1, f) == 1 && std::fwrite(&e->tm_learn, 4, 1, f) == 1;
+    std::vector<uint8_t> buf;
+    for (int id = 1; ok && id <= 16; id++) {
+        const Region& r = e->regions[id];
+        uint64_t nb = (uint64_t)r.per_stream * e->n;
+        buf.resize(nb);
+        if (htm_export_state(e, id, 0, e->n, buf.data(), nb)) { ok = false; break; }
+        int32_t rid = id;
+        ok = std::fwrite(&rid, 4, 1, f) == 1 && std::fwrite(&nb, 8, 1, f) == 1 && std::fwrite(buf.data(), 1, nb, f) == nb;
+    }
+    // last SP output (the TM of the next step does not need it, kept for outputs)
+    std::fclose(f);
+    if (!ok) return fail(HTM_E_IO, "write failed: %s", path);
+    return HTM_OK;
+}
+
+int htm_load(const char* path, int32_t device, htm_engine** out) {
+    if (!path || !out) return fail(HTM_E_INVALID, "bad arguments");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(HTM_E_IO, "cannot open %s", path);
+    char magic[8];
+    int32_t abi = 0, n = 0, spl = 1, tml = 1;
+    htm_config cfg;
+    bool ok = std::fread(magic, 8, 1, f) == 1 && std::memcmp(magic, "HTMAMD01", 8) == 0 &&
+              std::fread(&abi, 4, 1, f) == 1 && abi == HTM_ABI_VERSION &&
+              std::fread(&cfg, sizeof(cfg), 1, f) == 1 && std::fread(&n, 4, 1, f) == 1 &&
+              std::fread(&spl, 4, 1, f) == 1 && std::fread(&tml, 4, 1, f) == 1;
+    if (!ok) {
+        std::fclose(f);
+        return fail(HTM_E_IO, "%s is not an engine file of ABI %d", path, HTM_ABI_VERSION);
+    }
+    htm_engine* e = nullptr;
+    int r = create_uninit(&cfg, n, device, &e);
+    if (r) {
+        std::fclose(f);
+        return r;
+    }
+    std::vector<uint8_t> buf;
+    for (int k = 1; ok && k <= 16; k++) {
+        int32_t rid;
+        uint64_t nb;
+        ok = std::fread(&rid, 4, 1, f) == 1 && std::fread(&nb, 8, 1, f) == 1 && rid == k &&
+             nb == (uint64_t)e->regions[k].per_stream * n;
+        if (!ok) break;
+        buf.resize(nb);
+        ok = std::fread(buf.data(), 1, nb, f) == nb;
+        if (ok && htm_import_state(e, k, 0, n, buf.data(), nb)) ok = false;
+    }
+    std::fclose(f);
+    if (!ok) {
+        htm_destroy(e);
+        return fail(HTM_E_IO, "truncated or inconsistent engine file %s", path);
+    }
+    e->sp_learn = spl;
+    e->tm_learn = tml;
+    *out = e;
+    return HTM_OK;
+}
+
+}  // extern "C"

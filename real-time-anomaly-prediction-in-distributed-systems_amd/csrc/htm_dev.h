@@ -1,0 +1,228 @@
+// htm_dev.h -- device-side layout and helpers of the MI355X HTM engine.
+//
+// Memory is laid out per stream (structure-of-arrays per field, streams
+// contiguous), sized for 288 GB HBM: the SP keeps only potential synapses
+// (float32, potential order) plus an input-major connected bitmap, the TM a
+// slot-indexed segment pool (append-only; slot order == creation order, so
+// a cell's segment list order is slot order) and, while TM learning is off,
+// a forward index cell -> (segment, connected) used by frozen inference.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/htm_amd.h"
+
+#define HTM_MAXSYN 32     // synapse slots per TM segment
+#define HTM_MAXACT 64     // SP active columns (numActiveColumnsPerInhArea)
+#define HTM_MAXK 32       // cells per column
+#define HTM_MAXPAT 16     // backtrack pattern history slots
+#define HTM_NPLANES 7     // bit-sliced overlap planes (overlap <= 127)
+#define HTM_MAXNW 128     // ncol/32 words (ncol <= 4096)
+
+// Derived, immutable engine constants (kernel argument).
+struct DevCfg {
+    // encoder
+    int32_t n_fields, enc_n, enc_w, enc_clip;
+    double enc_min, enc_max, enc_resolution;
+    int32_t enc_halfwidth;
+    // SP
+    int32_t nin, nin_pad, ncol, nw;      // nw = ncol/32
+    int32_t n_potential;                  // potential synapses per column
+    int32_t num_desired;                  // winners per step
+    int32_t stim_thr, dc_period, update_period;
+    float sp_conn;                        // synPermConnected
+    float sp_conn_thr;                    // synPermConnected - PERMANENCE_EPSILON
+    float sp_inc, sp_dec, sp_trim, sp_below_inc, sp_min_pct_odc;
+    // TM
+    int32_t K, ncells, cw;                // cw = ncells/32
+    uint32_t kmagic;                      // ceil(2^32 / K): cell / K == umulhi(cell, kmagic)
+    int32_t new_syn, max_syn, max_segs_per_cell;
+    float init_perm, tm_conn, tm_inc, tm_dec, tm_max;
+    int32_t min_thr, act_thr, pam_len, max_inf_bt, max_lrn_bt, max_seq_len, upd_valid;
+    int32_t seg_cap, upd_cap;
+    int32_t seg_reserve;                  // free slots needed before a learning step
+    int32_t fx_win;                       // frozen index: segments per LDS counter window
+    int32_t fx_nwin;                      // windows covering seg_cap
+    int32_t n_streams;
+};
+
+// Device buffers (all per-stream strided).
+struct SpBufs {
+    uint32_t* connT;    // [S][nin_pad][nw]
+    uint32_t* potmask;  // [S][ncol][nin_pad/32]
+    float* perm;        // [S][ncol][n_potential]
+    float* duty;        // [S][2][ncol]: overlap dc, active dc
+    uint32_t* scalars;  // [S][4]: iter, iter_learn, min_odc bits, pad
+    uint16_t* act;      // [S][HTM_MAXACT] active columns (ascending)
+    uint32_t* nact;     // [S]
+    int32_t* overlaps;  // [S][ncol]
+    uint64_t* seeds;    // [S] SP seed per stream
+};
+
+struct TmBufs {
+    htm_tm_header* hdr;     // [S]
+    uint32_t* bm;           // [S][4][cw]: infA, infP, lrnA, lrnP (time t)
+    float* colconf;         // [S][ncol]
+    uint16_t* pat;          // [S][2*HTM_MAXPAT][HTM_MAXACT]: inf then lrn
+    uint32_t* seg_meta;     // [S][seg_cap]
+    uint16_t* seg_src;      // [S][seg_cap][32]
+    float* seg_perm;        // [S][seg_cap][32]
+    uint32_t* seg_conn;     // [S][seg_cap]
+    uint32_t* seg_duty;     // [S][seg_cap][3]: posAct, lastDC bits, lastDCIter
+    uint8_t* cell_nseg;     // [S][ncells]
+    htm_tm_update* upd;     // [S][upd_cap]
+    // scratch (per stream)
+    uint32_t* scr_bm;       // [S][5][cw]: infA backup, infP(t-1) backup, infA cand, infP cand, spare
+    float* scr_conf;        // [S][ncol]: colConf candidate
+    uint32_t* scr_q;        // [S][seg_cap]: qualifying segment keys
+    uint32_t* scr_q2;       // [S][seg_cap]: bucket-sorted keys
+    uint8_t* prev_pred;     // [S][ncol] nonzero(colConf(t-1)) captured before compute
+    uint32_t* scr_cur;      // [S][ncells*fx_nwin] frozen-index fill cursors
+    // frozen forward index (valid while TM learning is off): for stream s,
+    // cell x and counter window w the segment slots with a synapse from x
+    // are fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1])
+    uint64_t* fx_base;      // [S]
+    uint32_t* fx_off;       // [S][ncells][fx_nwin] + 1 (running, stream relative)
+    uint32_t* fx_ent;       // [total] segment slots
+};
+
+// ---------------------------------------------------------------------------
+// segment meta word
+__device__ __forceinline__ uint32_t meta_cell(uint32_t m) { return m & 0xFFFFu; }
+__device__ __forceinline__ uint32_t meta_nsyn(uint32_t m) { return (m >> 16) & 0x3Fu; }
+__device__ __forceinline__ uint32_t meta_seq(uint32_t m) { return (m >> 22) & 1u; }
+__device__ __forceinline__ uint32_t meta_live(uint32_t m) { return (m >> 23) & 1u; }
+__device__ __forceinline__ uint32_t make_meta(uint32_t cell, uint32_t nsyn, uint32_t seq, uint32_t live) {
+    return cell | (nsyn << 16) | (seq << 22) | (live << 23);
+}
+
+// ---------------------------------------------------------------------------
+// nupic::Random (BSD random() TYPE_3), state held in LDS or registers.
+struct Rng {
+    uint32_t s[31];
+    int32_t f, r;
+};
+
+__device__ __forceinline__ uint32_t rng_raw(uint32_t* s, int32_t& f, int32_t& r) {
+    s[f] += s[r];
+    uint32_t i = (s[f] >> 1) & 0x7fffffffu;
+    if (++f >= 31) { f = 0; ++r; }
+    else if (++r >= 31) { r = 0; }
+    return i;
+}
+
+__device__ __forceinline__ void rng_seed(uint32_t* s, int32_t& f, int32_t& r, uint64_t seed) {
+    int32_t x = (int32_t)(seed % 2147483646ull + 1ull);
+    s[0] = (uint32_t)x;
+    for (int i = 1; i < 31; i++) {
+        int32_t hi = x / 127773, lo = x % 127773;
+        x = 16807 * lo - 2836 * hi;
+        if (x < 0) x += 2147483647;
+        s[i] = (uint32_t)x;
+    }
+    f = 3;
+    r = 0;
+    for (int i = 0; i < 310; i++) (void)rng_raw(s, f, r);
+}
+
+// Random::getUInt32(max): raw draws are < 2^31 so the rejection never fires.
+__device__ __forceinline__ uint32_t rng_u32(uint32_t* s, int32_t& f, int32_t& r, uint32_t max) {
+    uint32_t smax = 0xFFFFFFFFu - (0xFFFFFFFFu % max);
+    uint32_t v;
+    do { v = rng_raw(s, f, r); } while (v > smax);
+    return v % max;
+}
+
+__device__ __forceinline__ double rng_real64(uint32_t* s, int32_t& f, int32_t& r) {
+    // getUInt64(2^48): lo | hi<<32, % 2^48 (never rejected)
+    uint64_t lo = rng_raw(s, f, r);
+    uint64_t hi = rng_raw(s, f, r);
+    uint64_t v = (lo | (hi << 32)) & ((1ull << 48) - 1ull);
+    return (double)v * (1.0 / 281474976710656.0);  // ldexp(v, -48), exact
+}
+
+// ---------------------------------------------------------------------------
+// bitmaps
+__device__ __forceinline__ bool bm_get(const uint32_t* bm, uint32_t i) { return (bm[i >> 5] >> (i & 31)) & 1u; }
+
+// bits [lo, lo+len) of a bitmap (len <= 32), returned in the low bits
+__device__ __forceinline__ uint32_t bm_field(const uint32_t* bm, uint32_t lo, uint32_t len) {
+    uint32_t w = lo >> 5, b = lo & 31;
+    uint64_t x = (uint64_t)bm[w];
+    if (b + len > 32) x |= (uint64_t)bm[w + 1] << 32;
+    x >>= b;
+    return (uint32_t)(x & ((len == 32) ? 0xFFFFFFFFull : ((1ull << len) - 1ull)));
+}
+
+// OR `bits` (len <= 32) into bitmap at [lo, lo+len) with LDS atomics
+__device__ __forceinline__ void bm_or_field(uint32_t* bm, uint32_t lo, uint32_t len, uint32_t bits) {
+    if (!bits) return;
+    uint32_t w = lo >> 5, b = lo & 31;
+    uint64_t x = (uint64_t)bits << b;
+    if ((uint32_t)x) atomicOr(&bm[w], (uint32_t)x);
+    if (b + len > 32 && (uint32_t)(x >> 32)) atomicOr(&bm[w + 1], (uint32_t)(x >> 32));
+}
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+// number of set bits of a 64-bit ballot below this lane
+__device__ __forceinline__ uint32_t ballot_rank(uint64_t ball) {
+    uint64_t m = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
+    return (uint32_t)__popcll(ball & m);
+}
+
+// pow(b, e) for integer e by binary exponentiation in double, rounded to
+// float: deterministic on host and device (the oracle uses the same rule).
+__device__ __forceinline__ float pow_det(float b, uint32_t e) {
+    double r = 1.0, x = (double)b;
+    while (e) {
+        if (e & 1u) r = __dmul_rn(r, x);
+        x = __dmul_rn(x, x);
+        e >>= 1;
+    }
+    return (float)r;
+}
+
+// host launch wrappers (defined in sp.hip / tm.hip)
+int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st);
+int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
+                   hipStream_t st);
+int launch_tm_init(const DevCfg& c, const TmBufs& b, const uint64_t* seeds, int n, hipStream_t st);
+int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen,
+                   int n, hipStream_t st);
+int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
+int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen);
+int tm_configure_lds(const DevCfg& c);
+int launch_prev_pred(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

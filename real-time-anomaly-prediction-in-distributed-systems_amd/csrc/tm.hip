@@ -1,0 +1,1487 @@
+// tm.hip -- BacktrackingTM (TMRegion, temporalImp "cpp") + raw anomaly for
+// N streams on gfx950, one 256-thread workgroup per stream per step.
+//
+// Reference path: TMRegion.compute -> BacktrackingTMCPP.compute -> Cells4
+// (params ML/HTM/NetworkUtils.py:44-64,140-153; anomaly read at
+// ML/HTM/NetworkModel.py:133).  Control flow restates NuPIC's BacktrackingTM
+// (updateInferenceState / inferPhase1 / inferPhase2 / inferBacktrack,
+// updateLearningState / learnPhase1 / learnPhase2 / learnBacktrack,
+// processSegmentUpdates, adaptSegment, getBestMatchingCell,
+// getCellForNewSegment, chooseCellsToLearnFrom) exactly as oracle/htm_oracle.c
+// does.
+//
+// MI355X design:
+//   * the whole step of one stream runs inside one workgroup: its bitmaps
+//     (cells x 1 bit), column confidences and bookkeeping live in LDS;
+//     segment state streams from HBM;
+//   * inference phase 2 (the hot loop) has two forms with identical results:
+//       - learning on:  a coalesced scan of the segment pool (4 lanes per
+//         segment, 16 B of synapse sources each) probing the LDS bitmap;
+//       - learning off: forward propagation over a frozen cell -> segment
+//         index (what Cells4's _outSynapses does), counting active synapses
+//         per segment with LDS atomics in windows of the slot space, so a
+//         step reads only the out-synapses of the active cells;
+//   * the float32 column confidences are summed in NuPIC's (column, cell,
+//     segment) order (bucket sort of the qualifying segments), so they are
+//     bit-identical to the oracle;
+//   * the data-dependent nupic::Random draws of learning run on lane 0 of
+//     wave 0 in NuPIC order; everything else is wave- or workgroup-parallel.
+#include "htm_dev.h"
+
+#define TM_NT 256
+#define TM_NWAVES (TM_NT / 64)
+
+__constant__ float kDcAlpha[9] = {0.0f, 0.0032f, 0.0010f, 0.00032f, 0.00010f, 0.000032f, 0.00001f, 0.0000032f, 0.0000010f};
+__constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 100000, 320000};
+
+struct __attribute__((aligned(16))) TmSh {
+    double avg_dens, avg_lsl;
+    uint32_t lrn_iter, iter;
+    int32_t pam, lsl, reset, have_avg;
+    uint32_t rng[31];
+    int32_t rf, rr;
+    uint32_t hwm, nlive;
+    int32_t n_inf_pat, n_lrn_pat, inf_head, lrn_head;
+    uint16_t inf_len[HTM_MAXPAT], lrn_len[HTM_MAXPAT];
+    int32_t n_upd;
+    uint32_t err;
+    uint32_t st[4];
+    int32_t nA;
+    int32_t qn;
+    int32_t ncand;
+    int32_t ti[8];
+    float tf[4];
+    uint32_t red[2 * TM_NWAVES];
+    uint16_t act[HTM_MAXACT];
+    uint32_t cand[HTM_MAXACT];
+    uint32_t newsrc[HTM_MAXSYN];
+    uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
+    uint16_t lrn_pat[HTM_MAXPAT][HTM_MAXACT];
+};
+
+struct Tm {
+    DevCfg c;
+    int s;
+    TmSh* sh;
+    // LDS regions
+    uint32_t *infA, *infP, *infP1, *lrnA, *lrnA1, *lrnP, *lrnP1;
+    float* colconf;
+    uint32_t* flags;   // ncol bits
+    uint32_t* U;       // union region
+    // global, this stream
+    uint32_t* meta;
+    uint16_t* src;
+    float* perm;
+    uint32_t* conn;
+    uint32_t* duty;
+    uint8_t* nseg;
+    htm_tm_update* upd;
+    uint32_t* sbm;     // scratch bitmaps [5][cw]
+    float* sconf;
+    uint32_t* q1;
+    uint32_t* q2;
+    const uint32_t* fxoff;
+    const uint32_t* fxent;
+};
+
+// ---------------------------------------------------------------------------
+// LDS layout
+struct TmLayout {
+    size_t off_bm, off_conf, off_flags, off_U, total;
+    int nbm;
+    size_t u_words;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int frozen) {
+    TmLayout L;
+    L.nbm = learn ? 7 : 3;
+    size_t o = align16(sizeof(TmSh));
+    L.off_bm = o;
+    o = align16(o + (size_t)L.nbm * c.cw * 4);
+    L.off_conf = o;
+    o = align16(o + (size_t)c.ncol * 4);
+    L.off_flags = o;
+    o = align16(o + (size_t)c.nw * 4);
+    L.off_U = o;
+    // union: finish (colcnt ncol + nzcol ncol/2 + nzstart ncol+1), keys (2 ncol),
+    // frozen collection (counters fx_win/4 + cell list 2048 u16), trim flags
+    size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1;
+    size_t keys = learn ? 2 * (size_t)c.ncol : 0;
+    size_t col = frozen ? (size_t)c.fx_win / 4 + 1024 : 0;
+    size_t trim = learn ? (size_t)c.upd_cap : 0;
+    size_t u = fin;
+    if (keys > u) u = keys;
+    if (col > u) u = col;
+    if (trim > u) u = trim;
+    L.u_words = u;
+    o = align16(o + u * 4);
+    L.total = o;
+    return L;
+}
+
+size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).total; }
+
+// ---------------------------------------------------------------------------
+// workgroup helpers
+__device__ __forceinline__ void wg_clear(uint32_t* p, int n) {
+    for (int i = threadIdx.x; i < n; i += TM_NT) p[i] = 0;
+}
+__device__ __forceinline__ void wg_copy(uint32_t* d, const uint32_t* s, int n) {
+    for (int i = threadIdx.x; i < n; i += TM_NT) d[i] = s[i];
+}
+// sum over the workgroup (contains barriers; call uniformly)
+__device__ __forceinline__ uint32_t wg_sum(TmSh* sh, uint32_t v) {
+    v = wave_sum_u32(v);
+    __syncthreads();
+    if (lane_id() == 0) sh->red[wave_id()] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < TM_NWAVES; w++) t += sh->red[w];
+    __syncthreads();
+    return t;
+}
+// exclusive prefix over the workgroup in thread order; *total gets the sum
+__device__ __forceinline__ uint32_t wg_excl_scan(TmSh* sh, uint32_t v, uint32_t* total) {
+    uint32_t incl = wave_incl_scan(v);
+    __syncthreads();
+    if (lane_id() == 63) sh->red[wave_id()] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < TM_NWAVES; w++) {
+        if (w < wave_id()) base += sh->red[w];
+        tot += sh->red[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + incl - v;
+}
+
+__device__ __forceinline__ uint32_t col_of(const DevCfg& c, uint32_t cell) { return __umulhi(cell, c.kmagic); }
+__device__ __forceinline__ uint32_t kmask(int K) { return K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u); }
+
+// Segment::dutyCycle(iteration, active, readOnly=false) on the pool entry
+__device__ float seg_dc_update(uint32_t* duty, uint32_t slot, uint32_t it, bool active) {
+    uint32_t* d = duty + (size_t)slot * 3;
+    float dc;
+    if (it <= kDcTier[1]) {
+        dc = (float)d[0] / (float)it;
+        d[1] = __float_as_uint(dc);
+        d[2] = it;
+        return dc;
+    }
+    uint32_t age = it - d[2];
+    float last = __uint_as_float(d[1]);
+    if (age == 0 && !active) return last;
+    float alpha = 0.0f;
+    for (int t = 8; t > 0; t--) {
+        if (it > kDcTier[t]) { alpha = kDcAlpha[t]; break; }
+    }
+    dc = pow_det((float)(1.0 - (double)alpha), age) * last;
+    if (active) dc += alpha;
+    d[1] = __float_as_uint(dc);
+    d[2] = it;
+    return dc;
+}
+
+// ---------------------------------------------------------------------------
+// cell list of a bitmap (ascending) into dst; returns count (uniform)
+__device__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, uint32_t* dst32, uint16_t* dst16, uint32_t cap) {
+    const int cw = t.c.cw;
+    const int per = (cw + TM_NT - 1) / TM_NT;
+    const int w0 = threadIdx.x * per;
+    uint32_t cnt = 0;
+    for (int k = 0; k < per; k++)
+        if (w0 + k < cw) cnt += __popc(bm[w0 + k]);
+    uint32_t total;
+    uint32_t pos = wg_excl_scan(t.sh, cnt, &total);
+    for (int k = 0; k < per; k++) {
+        int w = w0 + k;
+        if (w >= cw) break;
+        for (uint32_t x = bm[w]; x; x &= x - 1) {
+            uint32_t cell = (uint32_t)w * 32 + __ffs(x) - 1;
+            if (pos < cap) {
+                if (dst32) dst32[pos] = cell;
+                if (dst16) dst16[pos] = (uint16_t)cell;
+            }
+            pos++;
+        }
+    }
+    __syncthreads();
+    return total;
+}
+
+// ---------------------------------------------------------------------------
+// Inference
+// _inferPhase1(activeColumns, useStartCells)
+__device__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start) {
+    const int K = t.c.K;
+    wg_clear(t.infA, t.c.cw);
+    __syncthreads();
+    uint32_t npc = 0;
+    for (int a = threadIdx.x; a < nA; a += TM_NT) {
+        uint32_t lo = (uint32_t)cols[a] * K;
+        if (use_start) {
+            bm_or_field(t.infA, lo, 1, 1u);
+        } else {
+            uint32_t f = bm_field(t.infP1, lo, K);
+            if (f) {
+                bm_or_field(t.infA, lo, K, f);
+                npc++;
+            } else {
+                bm_or_field(t.infA, lo, K, kmask(K));
+            }
+        }
+    }
+    npc = wg_sum(t.sh, npc);
+    return use_start || (double)npc >= 0.50 * (double)nA;
+}
+
+// collect slots of segments with >= thr synapses onto active cells of
+// `state` by scanning the pool (learning-on form)
+__device__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
+    const uint32_t hwm = t.sh->hwm;
+    const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    for (uint32_t base = 0; base < hwm; base += TM_NT / 4) {
+        uint32_t slot = base + g;
+        uint32_t m = slot < hwm ? t.meta[slot] : 0u;
+        uint32_t nsyn = meta_nsyn(m);
+        bool live = meta_live(m);
+        uint32_t mask = 0;
+        if (live && (uint32_t)(sub * 8) < nsyn) {
+            uint4 v = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                uint32_t j = sub * 8 + k;
+                uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+                if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
+            }
+        }
+        mask |= __shfl_xor(mask, 1, 64);
+        mask |= __shfl_xor(mask, 2, 64);
+        if (live && sub == 0 && __popc(mask) >= thr) {
+            int i = atomicAdd(&t.sh->qn, 1);
+            t.q1[i] = slot;
+        }
+    }
+}
+
+// learning-off form: forward propagation over the frozen cell->segment index
+__device__ void collect_frozen(Tm& t, int thr) {
+    const DevCfg& c = t.c;
+    uint32_t* cnt = t.U;
+    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + c.fx_win / 4);
+    const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, 2048);
+    const uint32_t ncells_act = nact < 2048 ? nact : 2048;
+    const uint32_t hwm = t.sh->hwm;
+    const uint32_t W = (uint32_t)c.fx_win;
+    for (uint32_t w = 0; w * W < hwm; w++) {
+        wg_clear(cnt, (int)(W / 4));
+        __syncthreads();
+        for (uint32_t k = wave_id(); k < ncells_act; k += TM_NWAVES) {
+            const uint32_t* o = t.fxoff + (size_t)cells[k] * c.fx_nwin + w;
+            uint32_t lo = o[0], hi = o[1];
+            for (uint32_t e = lo + lane_id(); e < hi; e += 64) {
+                uint32_t rel = t.fxent[e] - w * W;
+                atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < W / 4; i += TM_NT) {
+            uint32_t x = cnt[i];
+            if (!x) continue;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if (((x >> (8 * b)) & 0xFFu) >= (uint32_t)thr) {
+                    int q = atomicAdd(&t.sh->qn, 1);
+                    t.q1[q] = w * W + 4 * i + b;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
+// NuPIC order, normalisation.  Returns numPredictedCols (uniform).
+__device__ uint32_t phase2_finish(Tm& t) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int K = c.K;
+    const uint32_t qn = (uint32_t)sh->qn;
+    uint32_t* colcnt = t.U;
+    uint16_t* nzcol = reinterpret_cast<uint16_t*>(t.U + c.ncol);
+    uint32_t* nzstart = t.U + c.ncol + (c.ncol + 1) / 2;
+    wg_clear(colcnt, c.ncol);
+    __syncthreads();
+    // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
+    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+        uint32_t slot = t.q1[k];
+        uint32_t m = t.meta[slot];
+        uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
+        uint32_t cm = t.conn[slot];
+        const uint4* row = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
+        uint32_t n = 0;
+        for (int q = 0; q < 4; q++) {
+            if ((uint32_t)q * 8 >= nsyn) break;
+            uint4 v = row[q];
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k2 = 0; k2 < 8; k2++) {
+                uint32_t j = q * 8 + k2;
+                uint32_t sid = (w[k2 >> 1] >> ((k2 & 1) * 16)) & 0xFFFFu;
+                if (j < nsyn && ((cm >> j) & 1u) && bm_get(t.infA, sid)) n++;
+            }
+        }
+        if (n >= (uint32_t)c.act_thr) atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
+        (void)seg_dc_update(t.duty, slot, sh->lrn_iter, false);
+        atomicAdd(&colcnt[col_of(c, cell)], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of bucket counts + nonzero column list (ascending)
+    const int per = (c.ncol + TM_NT - 1) / TM_NT;
+    const int c0 = threadIdx.x * per;
+    uint32_t lsum = 0, lnz = 0;
+    for (int k = 0; k < per; k++) {
+        int col = c0 + k;
+        if (col < c.ncol && colcnt[col]) { lsum += colcnt[col]; lnz++; }
+    }
+    uint32_t tsum, tnz;
+    uint32_t off = wg_excl_scan(sh, lsum, &tsum);
+    uint32_t zo = wg_excl_scan(sh, lnz, &tnz);
+    for (int k = 0; k < per; k++) {
+        int col = c0 + k;
+        if (col >= c.ncol) break;
+        uint32_t n = colcnt[col];
+        if (n) {
+            nzcol[zo] = (uint16_t)col;
+            nzstart[zo] = off;
+            zo++;
+        }
+        colcnt[col] = off;
+        off += n;
+    }
+    if (threadIdx.x == 0) nzstart[tnz] = tsum;
+    __syncthreads();
+    // pass 2: scatter keys (cellInColumn << 27 | slot) into column buckets
+    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+        uint32_t slot = t.q1[k];
+        uint32_t cell = meta_cell(t.meta[slot]);
+        uint32_t col = col_of(c, cell);
+        uint32_t pos = atomicAdd(&colcnt[col], 1u);
+        t.q2[pos] = ((cell - col * K) << 27) | slot;
+    }
+    __syncthreads();
+    // pass 3: per column, (cell, slot) order; float sum in that order
+    uint32_t npcol = 0;
+    for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) {
+        uint32_t col = nzcol[k], lo = nzstart[k], hi = nzstart[k + 1];
+        for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort (buckets are small)
+            uint32_t key = t.q2[i];
+            uint32_t j = i;
+            while (j > lo && t.q2[j - 1] > key) { t.q2[j] = t.q2[j - 1]; j--; }
+            t.q2[j] = key;
+        }
+        float sum = 0.0f;
+        for (uint32_t i = lo; i < hi; i++) {
+            uint32_t slot = t.q2[i] & 0x7FFFFFFu;
+            sum += __uint_as_float(t.duty[(size_t)slot * 3 + 1]);
+        }
+        t.colconf[col] = sum;
+        if (bm_field(t.infP, col * K, K)) npcol++;
+    }
+    npcol = wg_sum(sh, npcol);
+    if (threadIdx.x == 0) {
+        float tot = 0.0f;
+        for (uint32_t k = 0; k < tnz; k++) tot += t.colconf[nzcol[k]];
+        sh->tf[0] = tot;
+    }
+    __syncthreads();
+    float tot = sh->tf[0];
+    if (tot > 0.0f)
+        for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) t.colconf[nzcol[k]] /= tot;
+    __syncthreads();
+    return npcol;
+}
+
+// _inferPhase2()
+template <bool FROZEN>
+__device__ bool infer_phase2(Tm& t) {
+    TmSh* sh = t.sh;
+    if (threadIdx.x == 0) {
+        sh->st[0]++;
+        sh->qn = 0;
+    }
+    wg_clear(t.infP, t.c.cw);
+    wg_clear(reinterpret_cast<uint32_t*>(t.colconf), t.c.ncol);
+    __syncthreads();
+    if (FROZEN) collect_frozen(t, t.c.act_thr);
+    else collect_scan(t, t.infA, t.c.act_thr);
+    __syncthreads();
+    uint32_t npc = phase2_finish(t);
+    return (double)npc >= 0.5 * sh->avg_dens;
+}
+
+__device__ __forceinline__ const uint16_t* inf_pat(Tm& t, int k) {
+    return t.sh->inf_pat[(t.sh->inf_head + k) % HTM_MAXPAT];
+}
+__device__ __forceinline__ int inf_len(Tm& t, int k) { return t.sh->inf_len[(t.sh->inf_head + k) % HTM_MAXPAT]; }
+__device__ __forceinline__ const uint16_t* lrn_pat(Tm& t, int k) {
+    return t.sh->lrn_pat[(t.sh->lrn_head + k) % HTM_MAXPAT];
+}
+__device__ __forceinline__ int lrn_len(Tm& t, int k) { return t.sh->lrn_len[(t.sh->lrn_head + k) % HTM_MAXPAT]; }
+
+// _inferBacktrack(activeColumns)
+template <bool FROZEN>
+__device__ void infer_backtrack(Tm& t) {
+    TmSh* sh = t.sh;
+    const int cw = t.c.cw;
+    const int numPrev = sh->n_inf_pat;
+    if (numPrev <= 0) return;
+    const int cur = numPrev - 1;
+    if (threadIdx.x == 0) sh->st[1]++;
+    uint32_t* bkA = t.sbm;
+    uint32_t* bkP = t.sbm + cw;
+    uint32_t* cdA = t.sbm + 2 * cw;
+    uint32_t* cdP = t.sbm + 3 * cw;
+    wg_copy(bkA, t.infA, cw);
+    wg_copy(bkP, t.infP1, cw);
+    __syncthreads();
+    uint32_t bad = 0;
+    bool haveCand = false;
+    int candStart = -1;
+    for (int start = 0; start < numPrev; start++) {
+        if (start == cur && haveCand) break;
+        bool inSeq = false;
+        for (int off = start; off < numPrev; off++) {
+            wg_copy(t.infP1, t.infP, cw);
+            __syncthreads();
+            inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
+            if (!inSeq) break;
+            inSeq = infer_phase2<FROZEN>(t);
+            if (!inSeq) break;
+        }
+        if (!inSeq) {
+            bad |= 1u << start;
+            continue;
+        }
+        haveCand = true;
+        candStart = start;
+        if (candStart == cur) break;
+        wg_copy(cdA, t.infA, cw);
+        wg_copy(cdP, t.infP, cw);
+        wg_copy(reinterpret_cast<uint32_t*>(t.sconf), reinterpret_cast<const uint32_t*>(t.colconf), t.c.ncol);
+        __syncthreads();
+        break;
+    }
+    if (!haveCand) {
+        wg_copy(t.infA, bkA, cw);
+        __syncthreads();
+        (void)infer_phase2<FROZEN>(t);
+    } else if (candStart != cur) {
+        wg_copy(t.infA, cdA, cw);
+        wg_copy(t.infP, cdP, cw);
+        wg_copy(reinterpret_cast<uint32_t*>(t.colconf), reinterpret_cast<const uint32_t*>(t.sconf), t.c.ncol);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int npop = 0;
+        for (int i = 0; i < numPrev; i++) {
+            if (((bad >> i) & 1u) || (haveCand && i <= candStart)) npop++;
+            else break;
+        }
+        sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
+        sh->n_inf_pat -= npop;
+    }
+    wg_copy(t.infP1, bkP, cw);
+    __syncthreads();
+}
+
+// _updateInferenceState(activeColumns)
+template <bool FROZEN>
+__device__ void update_inference(Tm& t) {
+    TmSh* sh = t.sh;
+    if (threadIdx.x == 0) {
+        if (t.c.max_inf_bt > 0) {
+            if (sh->n_inf_pat > t.c.max_inf_bt) {
+                sh->inf_head = (sh->inf_head + 1) % HTM_MAXPAT;
+                sh->n_inf_pat--;
+            }
+            int slot = (sh->inf_head + sh->n_inf_pat) % HTM_MAXPAT;
+            sh->inf_len[slot] = (uint16_t)sh->nA;
+            sh->ti[0] = slot;
+            sh->n_inf_pat++;
+        } else {
+            sh->ti[0] = -1;
+        }
+    }
+    __syncthreads();
+    if (sh->ti[0] >= 0)
+        for (int a = threadIdx.x; a < sh->nA; a += TM_NT) sh->inf_pat[sh->ti[0]][a] = sh->act[a];
+    __syncthreads();
+    bool inSeq = infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
+    if (!inSeq) {
+        infer_backtrack<FROZEN>(t);
+        return;
+    }
+    inSeq = infer_phase2<FROZEN>(t);
+    if (!inSeq) infer_backtrack<FROZEN>(t);
+}
+
+// ---------------------------------------------------------------------------
+// Learning (wave-0 sequential helpers run with all 64 lanes of wave 0)
+
+// per-column best (activity, cellInColumn, first segment) key over the pool
+// for segments with >= thr synapses onto `state`; only columns flagged in
+// `colflags` when it is non-null.  _getBestMatchingCell for many columns.
+__device__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t* colflags) {
+    const DevCfg& c = t.c;
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
+    const uint32_t hwm = t.sh->hwm;
+    const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    for (uint32_t base = 0; base < hwm; base += TM_NT / 4) {
+        uint32_t slot = base + g;
+        uint32_t m = slot < hwm ? t.meta[slot] : 0u;
+        uint32_t nsyn = meta_nsyn(m), cell = meta_cell(m);
+        uint32_t col = col_of(c, cell);
+        bool elig = meta_live(m) && (!colflags || ((colflags[col >> 5] >> (col & 31)) & 1u));
+        uint32_t mask = 0;
+        if (elig && (uint32_t)(sub * 8) < nsyn) {
+            uint4 v = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                uint32_t j = sub * 8 + k;
+                uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+                if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
+            }
+        }
+        mask |= __shfl_xor(mask, 1, 64);
+        mask |= __shfl_xor(mask, 2, 64);
+        uint32_t n = __popc(mask);
+        if (elig && sub == 0 && n >= (uint32_t)thr) {
+            uint32_t cic = cell - col * c.K;
+            unsigned long long key = ((unsigned long long)n << 40) | ((unsigned long long)cic << 32) |
+                                     (unsigned long long)(0xFFFFFFFFu - slot);
+            atomicMax(&keys[col], key);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t key_slot(unsigned long long k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ __forceinline__ uint32_t key_cic(unsigned long long k) { return (uint32_t)(k >> 32) & 0xFFu; }
+__device__ __forceinline__ uint32_t key_act(unsigned long long k) { return (uint32_t)(k >> 40); }
+
+struct WUpd {
+    uint32_t mask;   // active existing synapse positions
+    uint32_t n_new;  // new sources
+    uint32_t my_new; // lane k (< n_new): k-th new source
+};
+
+// _getSegmentActiveSynapses(c, i, s, activeState, newSynapses) with
+// _chooseCellsToLearnFrom; candidates = sh->cand (cells on in `state`).
+// slot == 0xFFFFFFFF: new segment.
+__device__ WUpd w_build_update(Tm& t, uint32_t slot, const uint32_t* state, bool want_new) {
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    const bool exist = slot != 0xFFFFFFFFu;
+    uint32_t nsyn = exist ? meta_nsyn(t.meta[slot]) : 0u;
+    uint32_t mysrc = (exist && (uint32_t)l < nsyn) ? (uint32_t)t.src[(size_t)slot * HTM_MAXSYN + l] : 0xFFFFFFFFu;
+    bool act = (exist && (uint32_t)l < nsyn) && bm_get(state, mysrc);
+    WUpd u;
+    u.mask = (uint32_t)__ballot(act);
+    u.n_new = 0;
+    u.my_new = 0;
+    int n = want_new ? t.c.new_syn - __popc(u.mask) : 0;
+    if (n <= 0) return u;
+    const int ncand = sh->ncand;
+    uint32_t cv = l < ncand ? sh->cand[l] : 0xFFFFFFFEu;
+    bool ok = l < ncand;
+    for (uint32_t j = 0; j < nsyn; j++) {
+        uint32_t sj = __shfl(mysrc, (int)j, 64);
+        if (cv == sj) ok = false;
+    }
+    uint64_t keep = __ballot(ok);
+    const uint32_t m = (uint32_t)__popcll(keep);
+    if (m == 0) return u;
+    const uint32_t pos = ballot_rank(keep);
+    uint64_t chosen;
+    if (m <= (uint32_t)n) {
+        chosen = (m == 64) ? ~0ull : ((1ull << m) - 1ull);
+    } else {
+        uint64_t ch = 0;
+        if (l == 0) {
+            int32_t f = sh->rf, r = sh->rr;
+            if (n == 1) {
+                ch = 1ull << rng_u32(sh->rng, f, r, m);
+            } else {
+                uint32_t cnt = 0;
+                for (uint32_t i = 0; i < m; i++) {
+                    if (rng_u32(sh->rng, f, r, m - i) < (uint32_t)n - cnt) {
+                        ch |= 1ull << i;
+                        if (++cnt == (uint32_t)n) break;
+                    }
+                }
+            }
+            sh->rf = f;
+            sh->rr = r;
+        }
+        chosen = __shfl(ch, 0, 64);
+    }
+    if (ok && ((chosen >> pos) & 1ull)) {
+        uint32_t op = (uint32_t)__popcll(chosen & ((1ull << pos) - 1ull));
+        sh->newsrc[op] = cv;
+    }
+    u.n_new = (uint32_t)__popcll(chosen);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    u.my_new = (uint32_t)l < u.n_new ? sh->newsrc[l] : 0u;
+    return u;
+}
+
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+    return v;
+}
+
+// _adaptSegment on an existing segment; returns trimSegment (wave-uniform)
+__device__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t n_new, uint32_t my_new) {
+    const DevCfg& c = t.c;
+    const int l = lane_id();
+    const uint32_t m = t.meta[slot];
+    const uint32_t nsyn = meta_nsyn(m);
+    uint16_t* srow = t.src + (size_t)slot * HTM_MAXSYN;
+    float* prow = t.perm + (size_t)slot * HTM_MAXSYN;
+    if (l == 0) {
+        t.duty[(size_t)slot * 3] += 1u;  // positiveActivations
+        (void)seg_dc_update(t.duty, slot, t.sh->lrn_iter, true);
+    }
+    const bool in = (uint32_t)l < nsyn;
+    uint32_t sj = in ? srow[l] : 0u;
+    float p = in ? prow[l] : 0.0f;
+    const bool isact = in && ((amask >> l) & 1u);
+    const bool inact = in && !isact;
+    bool hit0 = false;
+    if (inact) {
+        float nv = p + (-c.tm_dec);
+        p = nv;
+        if (nv <= 0.0f) { p = 0.0f; hit0 = true; }
+    }
+    if (isact) {
+        float nv = p + c.tm_inc;
+        p = nv;
+        if (nv > c.tm_max) p = c.tm_max;
+    }
+    const bool trim = __ballot(hit0) != 0ull;
+    bool del = false;
+    if (nsyn + n_new > (uint32_t)c.max_syn) {
+        const uint32_t numToFree = nsyn + n_new - (uint32_t)c.max_syn;
+        uint32_t rin = 0, rac = 0;
+        for (int k = 0; k < 32; k++) {
+            float pk = __shfl(p, k, 64);
+            int ik = __shfl((int)inact, k, 64);
+            int ak = __shfl((int)isact, k, 64);
+            bool lt = (pk < p) || (pk == p && k < l);
+            if (ik && lt) rin++;
+            if (ak && lt) rac++;
+        }
+        const uint32_t ninact = (uint32_t)__popcll(__ballot(inact));
+        if (inact && rin < numToFree) del = true;
+        if (numToFree > ninact && isact && rac < numToFree - ninact) del = true;
+    }
+    const bool keep = in && !del;
+    const uint64_t kb = __ballot(keep);
+    const uint32_t nkeep = (uint32_t)__popcll(kb);
+    const uint32_t np = ballot_rank(kb);
+    uint32_t cbits = 0;
+    if (keep) {
+        srow[np] = (uint16_t)sj;
+        prow[np] = p;
+        if (p >= c.tm_conn) cbits |= 1u << np;
+    }
+    if ((uint32_t)l < n_new) {
+        srow[nkeep + l] = (uint16_t)my_new;
+        prow[nkeep + l] = c.init_perm;
+        if (c.init_perm >= c.tm_conn) cbits |= 1u << (nkeep + l);
+    }
+    cbits = wave_or_u32(cbits);
+    if (l == 0) {
+        t.conn[slot] = cbits;
+        t.meta[slot] = (m & ~(0x3Fu << 16)) | ((nkeep + n_new) << 16);
+    }
+    return trim;
+}
+
+// _trimSegmentsInCell(c, i, [s], minPermanence=0.00001, minNumSyns=0)
+__device__ void w_trim_segment(Tm& t, uint32_t slot) {
+    const DevCfg& c = t.c;
+    const int l = lane_id();
+    const uint32_t m = t.meta[slot];
+    const uint32_t nsyn = meta_nsyn(m), cell = meta_cell(m);
+    uint16_t* srow = t.src + (size_t)slot * HTM_MAXSYN;
+    float* prow = t.perm + (size_t)slot * HTM_MAXSYN;
+    const bool in = (uint32_t)l < nsyn;
+    uint32_t sj = in ? srow[l] : 0u;
+    float p = in ? prow[l] : 0.0f;
+    const bool del = in && p < 0.00001f;
+    const uint32_t ndel = (uint32_t)__popcll(__ballot(del));
+    if (ndel == nsyn) {
+        if (l == 0) {
+            t.meta[slot] = m & ~(1u << 23);
+            t.nseg[cell] -= 1;
+            atomicSub(&t.sh->nlive, 1u);
+        }
+        return;
+    }
+    if (ndel == 0) return;
+    const bool keep = in && !del;
+    const uint64_t kb = __ballot(keep);
+    const uint32_t np = ballot_rank(kb);
+    uint32_t cbits = 0;
+    if (keep) {
+        srow[np] = (uint16_t)sj;
+        prow[np] = p;
+        if (p >= c.tm_conn) cbits |= 1u << np;
+    }
+    cbits = wave_or_u32(cbits);
+    if (l == 0) {
+        t.conn[slot] = cbits;
+        t.meta[slot] = (m & ~(0x3Fu << 16)) | ((nsyn - ndel) << 16);
+    }
+}
+
+// new sequence segment on `cell` with the chosen sources
+__device__ void w_create_segment(Tm& t, uint32_t cell, uint32_t n_new, uint32_t my_new) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    uint32_t slot = sh->hwm;
+    if (slot >= (uint32_t)c.seg_cap) {
+        if (l == 0) sh->err |= 1u;
+        return;
+    }
+    if ((uint32_t)l < n_new) {
+        t.src[(size_t)slot * HTM_MAXSYN + l] = (uint16_t)my_new;
+        t.perm[(size_t)slot * HTM_MAXSYN + l] = c.init_perm;
+    }
+    if (l == 0) {
+        uint32_t cm = 0;
+        if (c.init_perm >= c.tm_conn) cm = n_new >= 32 ? 0xFFFFFFFFu : ((1u << n_new) - 1u);
+        t.conn[slot] = cm;
+        t.meta[slot] = make_meta(cell, n_new, 1u, 1u);
+        uint32_t* d = t.duty + (size_t)slot * 3;
+        d[0] = 1u;
+        d[1] = __float_as_uint((float)(1.0 / (double)sh->lrn_iter));
+        d[2] = sh->lrn_iter;
+        t.nseg[cell] += 1;
+        sh->hwm = slot + 1;
+        sh->nlive += 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// _getCellForNewSegment(colIdx); returns the cell index within the column
+__device__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    const int K = c.K;
+    const int minIdx = K == 1 ? 0 : 1, maxIdx = K == 1 ? 0 : K - 1;
+    bool ok = l >= minIdx && l <= maxIdx && (int)t.nseg[col * K + l] < c.max_segs_per_cell;
+    uint64_t b = __ballot(ok);
+    uint32_t m = (uint32_t)__popcll(b);
+    if (m > 0) {
+        uint32_t idx = 0;
+        if (l == 0) {
+            int32_t f = sh->rf, r = sh->rr;
+            idx = rng_u32(sh->rng, f, r, m);
+            sh->rf = f;
+            sh->rr = r;
+        }
+        idx = __shfl(idx, 0, 64);
+        // position of the idx-th set bit of b
+        uint64_t x = b;
+        for (uint32_t k = 0; k < idx; k++) x &= x - 1ull;
+        return (uint32_t)(__ffsll((unsigned long long)x) - 1);
+    }
+    // all cells full: free the least-used segment of the column
+    unsigned long long best = ~0ull;
+    const uint32_t hwm = sh->hwm;
+    for (uint32_t slot = l; slot < hwm; slot += 64) {
+        uint32_t mm = t.meta[slot];
+        if (!meta_live(mm)) continue;
+        uint32_t cell = meta_cell(mm);
+        if (col_of(c, cell) != col) continue;
+        uint32_t cic = cell - col * K;
+        if ((int)cic < minIdx) continue;
+        float dc = seg_dc_update(t.duty, slot, sh->lrn_iter, false);
+        unsigned long long key = ((unsigned long long)__float_as_uint(dc) << 32) | ((unsigned long long)cic << 27) | slot;
+        best = key < best ? key : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long tt = __shfl_xor(best, o, 64);
+        best = tt < best ? tt : best;
+    }
+    if (best == ~0ull || __uint_as_float((uint32_t)(best >> 32)) >= 1.0f) return (uint32_t)minIdx;
+    uint32_t slot = (uint32_t)best & 0x7FFFFFFu;
+    uint32_t cic = (uint32_t)(best >> 27) & 0x1Fu;
+    if (l == 0) {
+        uint32_t mm = t.meta[slot];
+        t.meta[slot] = mm & ~(1u << 23);
+        t.nseg[meta_cell(mm)] -= 1;
+        sh->nlive -= 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return cic;
+}
+
+// cells on in `bm` -> sh->cand (<= HTM_MAXACT, ascending)
+__device__ void build_cand(Tm& t, const uint32_t* bm) {
+    uint32_t n = wg_bitmap_list(t, bm, t.sh->cand, nullptr, HTM_MAXACT);
+    if (threadIdx.x == 0) {
+        if (n > HTM_MAXACT) { t.sh->err |= 8u; n = HTM_MAXACT; }
+        t.sh->ncand = (int32_t)n;
+    }
+    __syncthreads();
+}
+
+// _processSegmentUpdates(activeColumns)
+__device__ void process_segment_updates(Tm& t, const uint16_t* cols, int nA) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    wg_clear(t.flags, c.nw);
+    __syncthreads();
+    for (int a = threadIdx.x; a < nA; a += TM_NT) atomicOr(&t.flags[cols[a] >> 5], 1u << (cols[a] & 31));
+    __syncthreads();
+    const int n = sh->n_upd;
+    uint32_t* tflag = t.U;
+    for (int k = wave_id(); k < n; k += TM_NWAVES) {
+        const htm_tm_update& e = t.upd[k];
+        uint32_t col = e.col;
+        bool doit = ((t.flags[col >> 5] >> (col & 31)) & 1u) && (sh->lrn_iter - e.date <= (uint32_t)c.upd_valid);
+        bool trim = false;
+        if (doit) {
+            uint32_t nn = e.n_new;
+            uint32_t my_new = (uint32_t)lane_id() < nn ? e.new_src[lane_id()] : 0u;
+            trim = w_adapt_existing(t, e.slot, e.active_mask, nn, my_new);
+        }
+        if (lane_id() == 0) tflag[k] = trim ? 1u : 0u;
+    }
+    __syncthreads();
+    for (int k = wave_id(); k < n; k += TM_NWAVES)
+        if (tflag[k]) w_trim_segment(t, t.upd[k].slot);
+    __syncthreads();
+    if (threadIdx.x == 0) sh->n_upd = 0;
+    __syncthreads();
+}
+
+// _learnPhase1(activeColumns, readOnly)
+__device__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA, bool ro) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int K = c.K;
+    wg_clear(t.lrnA, c.cw);
+    wg_clear(t.flags, c.nw);
+    __syncthreads();
+    uint32_t nun = 0;
+    for (int a = threadIdx.x; a < nA; a += TM_NT) {
+        uint32_t col = cols[a];
+        uint32_t f = bm_field(t.lrnP1, col * K, K);
+        int pc = __popc(f);
+        if (pc == 1) {
+            bm_or_field(t.lrnA, col * K, K, f);
+        } else {
+            nun++;
+            atomicOr(&t.flags[col >> 5], 1u << (col & 31));
+            if (pc > 1) atomicOr(&sh->err, 4u);
+        }
+    }
+    nun = wg_sum(sh, nun);
+    const bool inSeq = (int)nun < nA / 2;
+    if (ro || nun == 0) return inSeq;
+    wg_clear(t.U, 2 * c.ncol);
+    __syncthreads();
+    scan_best(t, t.lrnA1, c.min_thr, t.flags);
+    __syncthreads();
+    build_cand(t, t.lrnA1);
+    const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
+    if (wave_id() == 0) {
+        for (int a = 0; a < nA; a++) {
+            uint32_t col = cols[a];
+            if (!((t.flags[col >> 5] >> (col & 31)) & 1u)) continue;
+            unsigned long long key = keys[col];
+            bool seqseg = false;
+            uint32_t slot = 0, cic = 0;
+            if (key) {
+                slot = key_slot(key);
+                cic = key_cic(key);
+                seqseg = meta_seq(t.meta[slot]) != 0u;
+            }
+            if (key && seqseg) {
+                if (lane_id() == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
+                WUpd u = w_build_update(t, slot, t.lrnA1, true);
+                bool trim = w_adapt_existing(t, slot, u.mask, u.n_new, u.my_new);
+                if (trim) w_trim_segment(t, slot);
+            } else {
+                cic = w_cell_for_new_segment(t, col);
+                if (lane_id() == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
+                WUpd u = w_build_update(t, 0xFFFFFFFFu, t.lrnA1, true);
+                w_create_segment(t, col * K + cic, u.n_new, u.my_new);
+            }
+        }
+    }
+    __syncthreads();
+    return inSeq;
+}
+
+// _learnPhase2(readOnly)
+__device__ void learn_phase2(Tm& t, bool ro) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int K = c.K;
+    if (threadIdx.x == 0) sh->st[2]++;
+    wg_clear(t.lrnP, c.cw);
+    wg_clear(t.U, 2 * c.ncol);
+    __syncthreads();
+    scan_best(t, t.lrnA, c.act_thr, nullptr);
+    __syncthreads();
+    const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
+    for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
+        unsigned long long key = keys[col];
+        if (key) bm_or_field(t.lrnP, (uint32_t)col * K + key_cic(key), 1, 1u);
+    }
+    __syncthreads();
+    if (ro) return;
+    build_cand(t, t.lrnA);
+    if (wave_id() == 0) {
+        for (int base = 0; base < c.ncol; base += 64) {
+            uint64_t b = __ballot(keys[base + lane_id()] != 0ull);
+            while (b) {
+                int bit = __ffsll((unsigned long long)b) - 1;
+                b &= b - 1ull;
+                uint32_t col = (uint32_t)(base + bit);
+                unsigned long long key = keys[col];
+                uint32_t slot = key_slot(key), act = key_act(key);
+                WUpd u = w_build_update(t, slot, t.lrnA, act < (uint32_t)c.new_syn);
+                if (u.mask == 0u && u.n_new == 0u) continue;
+                int idx = sh->n_upd;
+                if (idx >= c.upd_cap) {
+                    if (lane_id() == 0) sh->err |= 2u;
+                    continue;
+                }
+                htm_tm_update& e = t.upd[idx];
+                if ((uint32_t)lane_id() < u.n_new) e.new_src[lane_id()] = (uint16_t)u.my_new;
+                if (lane_id() == 0) {
+                    e.slot = slot;
+                    e.col = (uint16_t)col;
+                    e.cell = (uint8_t)key_cic(key);
+                    e.n_new = (uint8_t)u.n_new;
+                    e.active_mask = u.mask;
+                    e.date = sh->lrn_iter;
+                    sh->n_upd = idx + 1;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// start cells (cell 0) of the given columns into lrnA
+__device__ void set_start_cells(Tm& t, uint32_t* bm, const uint16_t* cols, int nA) {
+    wg_clear(bm, t.c.cw);
+    __syncthreads();
+    for (int a = threadIdx.x; a < nA; a += TM_NT) bm_or_field(bm, (uint32_t)cols[a] * t.c.K, 1, 1u);
+    __syncthreads();
+}
+
+// _learnBacktrackFrom(startOffset, readOnly)
+__device__ bool learn_backtrack_from(Tm& t, int start, bool ro) {
+    TmSh* sh = t.sh;
+    const int cw = t.c.cw;
+    const int numPrev = sh->n_lrn_pat;
+    const int cur = numPrev - 1;
+    if (!ro) {
+        if (threadIdx.x == 0) sh->n_upd = 0;
+        __syncthreads();
+    }
+    bool inSeq = true;
+    for (int off = start; off < numPrev; off++) {
+        wg_copy(t.lrnP1, t.lrnP, cw);
+        wg_copy(t.lrnA1, t.lrnA, cw);
+        __syncthreads();
+        const uint16_t* pat = lrn_pat(t, off);
+        const int len = lrn_len(t, off);
+        if (!ro) process_segment_updates(t, pat, len);
+        if (off == start) {
+            set_start_cells(t, t.lrnA, pat, len);
+            inSeq = true;
+        } else {
+            inSeq = learn_phase1(t, pat, len, ro);
+        }
+        if (!inSeq || off == cur) break;
+        learn_phase2(t, ro);
+    }
+    return inSeq;
+}
+
+// _learnBacktrack(): steps backtracked, 0 on failure
+__device__ int learn_backtrack(Tm& t) {
+    TmSh* sh = t.sh;
+    const int numPrev = sh->n_lrn_pat - 1;
+    if (numPrev <= 0) return 0;
+    if (threadIdx.x == 0) sh->st[3]++;
+    uint32_t bad = 0;
+    bool inSeq = false;
+    int start;
+    for (start = 0; start < numPrev; start++) {
+        inSeq = learn_backtrack_from(t, start, true);
+        if (inSeq) break;
+        bad |= 1u << start;
+    }
+    if (!inSeq) {
+        if (threadIdx.x == 0) sh->n_lrn_pat = 0;
+        __syncthreads();
+        return 0;
+    }
+    (void)learn_backtrack_from(t, start, false);
+    if (threadIdx.x == 0) {
+        int npop = 0;
+        for (int i = 0; i < numPrev; i++) {
+            if (((bad >> i) & 1u) || i <= start) npop++;
+            else break;
+        }
+        sh->lrn_head = (sh->lrn_head + npop) % HTM_MAXPAT;
+        sh->n_lrn_pat -= npop;
+    }
+    __syncthreads();
+    return numPrev - start;
+}
+
+// _updateLearningState(activeColumns)
+__device__ void update_learning(Tm& t) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    // lrnA1 / lrnP1 hold time t-1 (loaded at entry)
+    if (threadIdx.x == 0) {
+        if (c.max_lrn_bt > 0) {
+            if (sh->n_lrn_pat > c.max_lrn_bt) {
+                sh->lrn_head = (sh->lrn_head + 1) % HTM_MAXPAT;
+                sh->n_lrn_pat--;
+            }
+            int slot = (sh->lrn_head + sh->n_lrn_pat) % HTM_MAXPAT;
+            sh->lrn_len[slot] = (uint16_t)sh->nA;
+            sh->ti[1] = slot;
+            sh->n_lrn_pat++;
+        } else {
+            sh->ti[1] = -1;
+        }
+    }
+    __syncthreads();
+    if (sh->ti[1] >= 0)
+        for (int a = threadIdx.x; a < sh->nA; a += TM_NT) sh->lrn_pat[sh->ti[1]][a] = sh->act[a];
+    __syncthreads();
+    process_segment_updates(t, sh->act, sh->nA);
+    if (threadIdx.x == 0) {
+        if (sh->pam > 0) sh->pam--;
+        sh->lsl++;
+    }
+    __syncthreads();
+    if (!sh->reset) {
+        bool inSeq = learn_phase1(t, sh->act, sh->nA, false);
+        if (inSeq && threadIdx.x == 0) sh->pam = c.pam_len;
+        __syncthreads();
+    }
+    if (sh->reset || sh->pam == 0 || (c.max_seq_len != 0 && sh->lsl >= c.max_seq_len)) {
+        if (threadIdx.x == 0) {
+            int seqLength = sh->pam == 0 ? sh->lsl - c.pam_len : sh->lsl;
+            double alpha = sh->lrn_iter < 100 ? 0.5 : 0.1;
+            sh->avg_lsl = (1.0 - alpha) * sh->avg_lsl + alpha * (double)seqLength;
+        }
+        __syncthreads();
+        int backSteps = 0;
+        if (!sh->reset) backSteps = learn_backtrack(t);
+        if (sh->reset || backSteps == 0) {
+            backSteps = 0;
+            set_start_cells(t, t.lrnA, sh->act, sh->nA);
+            if (threadIdx.x == 0) sh->n_lrn_pat = 0;
+        }
+        if (threadIdx.x == 0) {
+            sh->pam = c.pam_len;
+            sh->lsl = backSteps;
+            sh->n_upd = 0;
+        }
+        __syncthreads();
+    }
+    learn_phase2(t, false);
+}
+
+// stable compaction of live segments (slot order preserved) so that a
+// learning step always has seg_reserve free slots
+__device__ void compact_pool(Tm& t) {
+    TmSh* sh = t.sh;
+    const uint32_t hwm = sh->hwm;
+    uint32_t base = 0;
+    // pass 1: new slot of every live segment -> q1
+    for (uint32_t c0 = 0; c0 < hwm; c0 += TM_NT) {
+        uint32_t slot = c0 + threadIdx.x;
+        bool live = slot < hwm && meta_live(t.meta[slot]);
+        uint32_t tot;
+        uint32_t pos = wg_excl_scan(sh, live ? 1u : 0u, &tot);
+        if (slot < hwm) t.q1[slot] = live ? base + pos : 0xFFFFFFFFu;
+        base += tot;
+    }
+    __syncthreads();
+    // pass 2: move in increasing slot order (destinations never exceed sources)
+    for (uint32_t c0 = 0; c0 < hwm; c0 += TM_NT) {
+        uint32_t slot = c0 + threadIdx.x;
+        uint32_t ns = slot < hwm ? t.q1[slot] : 0xFFFFFFFFu;
+        uint32_t mm = 0, cm = 0, d0 = 0, d1 = 0, d2 = 0;
+        uint4 sv[4];
+        float4 pv[8];
+        if (ns != 0xFFFFFFFFu) {
+            mm = t.meta[slot];
+            cm = t.conn[slot];
+            d0 = t.duty[(size_t)slot * 3];
+            d1 = t.duty[(size_t)slot * 3 + 1];
+            d2 = t.duty[(size_t)slot * 3 + 2];
+            const uint4* sr = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
+            const float4* pr = reinterpret_cast<const float4*>(t.perm + (size_t)slot * HTM_MAXSYN);
+#pragma unroll
+            for (int k = 0; k < 4; k++) sv[k] = sr[k];
+#pragma unroll
+            for (int k = 0; k < 8; k++) pv[k] = pr[k];
+        }
+        __syncthreads();
+        if (ns != 0xFFFFFFFFu && ns != slot) {
+            t.meta[ns] = mm;
+            t.conn[ns] = cm;
+            t.duty[(size_t)ns * 3] = d0;
+            t.duty[(size_t)ns * 3 + 1] = d1;
+            t.duty[(size_t)ns * 3 + 2] = d2;
+            uint4* sw = reinterpret_cast<uint4*>(t.src + (size_t)ns * HTM_MAXSYN);
+            float4* pw = reinterpret_cast<float4*>(t.perm + (size_t)ns * HTM_MAXSYN);
+#pragma unroll
+            for (int k = 0; k < 4; k++) sw[k] = sv[k];
+#pragma unroll
+            for (int k = 0; k < 8; k++) pw[k] = pv[k];
+        }
+        __syncthreads();
+    }
+    // queued updates follow their segments
+    for (int k = threadIdx.x; k < sh->n_upd; k += TM_NT) t.upd[k].slot = t.q1[t.upd[k].slot];
+    for (uint32_t slot = base + threadIdx.x; slot < hwm; slot += TM_NT) t.meta[slot] = 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) sh->hwm = base;
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+template <bool LEARN, bool FROZEN>
+__global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBufs sp, float* scores, int keep_prev) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int s = blockIdx.x;
+    const TmLayout L = tm_layout(c, LEARN, FROZEN);
+    Tm t;
+    t.c = c;
+    t.s = s;
+    t.sh = reinterpret_cast<TmSh*>(lds);
+    uint32_t* bmr = reinterpret_cast<uint32_t*>(lds + L.off_bm);
+    t.infA = bmr;
+    t.infP = bmr + c.cw;
+    t.infP1 = bmr + 2 * c.cw;
+    t.lrnA = LEARN ? bmr + 3 * c.cw : nullptr;
+    t.lrnA1 = LEARN ? bmr + 4 * c.cw : nullptr;
+    t.lrnP = LEARN ? bmr + 5 * c.cw : nullptr;
+    t.lrnP1 = LEARN ? bmr + 6 * c.cw : nullptr;
+    t.colconf = reinterpret_cast<float*>(lds + L.off_conf);
+    t.flags = reinterpret_cast<uint32_t*>(lds + L.off_flags);
+    t.U = reinterpret_cast<uint32_t*>(lds + L.off_U);
+    const size_t sc = (size_t)c.seg_cap;
+    t.meta = b.seg_meta + (size_t)s * sc;
+    t.src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
+    t.perm = b.seg_perm + (size_t)s * sc * HTM_MAXSYN;
+    t.conn = b.seg_conn + (size_t)s * sc;
+    t.duty = b.seg_duty + (size_t)s * sc * 3;
+    t.nseg = b.cell_nseg + (size_t)s * c.ncells;
+    t.upd = b.upd + (size_t)s * c.upd_cap;
+    t.sbm = b.scr_bm + (size_t)s * 5 * c.cw;
+    t.sconf = b.scr_conf + (size_t)s * c.ncol;
+    t.q1 = b.scr_q + (size_t)s * sc;
+    t.q2 = b.scr_q2 + (size_t)s * sc;
+    if (FROZEN) {
+        t.fxoff = b.fx_off + (size_t)s * ((size_t)c.ncells * c.fx_nwin + 1);
+        t.fxent = b.fx_ent + b.fx_base[s];
+    } else {
+        t.fxoff = nullptr;
+        t.fxent = nullptr;
+    }
+    TmSh* sh = t.sh;
+    htm_tm_header* hdr = b.hdr + s;
+    uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
+    float* gconf = b.colconf + (size_t)s * c.ncol;
+    uint16_t* gpat = b.pat + (size_t)s * 2 * HTM_MAXPAT * HTM_MAXACT;
+    // ---- load state
+    if (threadIdx.x == 0) {
+        sh->avg_dens = hdr->avg_input_density;
+        sh->avg_lsl = hdr->avg_learned_seq_length;
+        sh->lrn_iter = hdr->lrn_iter;
+        sh->iter = hdr->iter;
+        sh->pam = hdr->pam_counter;
+        sh->lsl = hdr->learned_seq_length;
+        sh->reset = hdr->reset_called;
+        sh->have_avg = hdr->have_avg_density;
+        sh->rf = hdr->rng_f;
+        sh->rr = hdr->rng_r;
+        sh->hwm = hdr->seg_hwm;
+        sh->nlive = hdr->seg_live;
+        sh->n_inf_pat = hdr->n_inf_pat;
+        sh->n_lrn_pat = hdr->n_lrn_pat;
+        sh->inf_head = hdr->inf_pat_head;
+        sh->lrn_head = hdr->lrn_pat_head;
+        sh->n_upd = hdr->n_upd;
+        sh->err = hdr->error;
+        sh->st[0] = hdr->stat_inf_phase2;
+        sh->st[1] = hdr->stat_inf_backtrack;
+        sh->st[2] = hdr->stat_lrn_phase2;
+        sh->st[3] = hdr->stat_lrn_backtrack;
+        uint32_t na = sp.nact[s];
+        sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
+    }
+    if (threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
+    if (threadIdx.x < HTM_MAXPAT) {
+        sh->inf_len[threadIdx.x] = hdr->inf_pat_len[threadIdx.x];
+        sh->lrn_len[threadIdx.x] = hdr->lrn_pat_len[threadIdx.x];
+    }
+    for (int i = threadIdx.x; i < HTM_MAXPAT * HTM_MAXACT; i += TM_NT) {
+        (&sh->inf_pat[0][0])[i] = gpat[i];
+        (&sh->lrn_pat[0][0])[i] = gpat[HTM_MAXPAT * HTM_MAXACT + i];
+    }
+    if (threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
+    wg_copy(t.infP1, gbm + c.cw, c.cw);   // infPredictedState t -> t-1
+    wg_copy(t.infP, gbm + c.cw, c.cw);
+    if (LEARN) {
+        wg_copy(t.lrnA1, gbm + 2 * c.cw, c.cw);  // lrnActiveState t -> t-1
+        wg_copy(t.lrnP1, gbm + 3 * c.cw, c.cw);  // lrnPredictedState t -> t-1
+        wg_copy(t.lrnA, gbm + 2 * c.cw, c.cw);
+        wg_copy(t.lrnP, gbm + 3 * c.cw, c.cw);
+    }
+    __syncthreads();
+    const int nA = sh->nA;
+    // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1))
+    uint32_t hit = 0;
+    for (int a = threadIdx.x; a < nA; a += TM_NT) hit += gconf[sh->act[a]] != 0.0f ? 1u : 0u;
+    if (keep_prev)
+        for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
+            b.prev_pred[(size_t)s * c.ncol + col] = gconf[col] != 0.0f ? 1 : 0;
+    hit = wg_sum(sh, hit);
+    if (threadIdx.x == 0) {
+        // computeRawAnomalyScore -> Real32 output
+        scores[s] = nA > 0 ? (float)((double)(nA - (int)hit) / (double)nA) : 0.0f;
+        if (LEARN) sh->lrn_iter++;
+        sh->iter++;
+        if (!sh->have_avg) {
+            sh->avg_dens = (double)nA;
+            sh->have_avg = 1;
+        } else {
+            sh->avg_dens = 0.99 * sh->avg_dens + 0.01 * (double)nA;
+        }
+    }
+    __syncthreads();
+    if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) compact_pool(t);
+    // ---- BacktrackingTM.compute(input, learn, infer=True)
+    update_inference<FROZEN>(t);
+    if (LEARN) update_learning(t);
+    // ---- write back
+    __syncthreads();
+    wg_copy(gbm, t.infA, c.cw);
+    wg_copy(gbm + c.cw, t.infP, c.cw);
+    if (LEARN) {
+        wg_copy(gbm + 2 * c.cw, t.lrnA, c.cw);
+        wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
+    }
+    wg_copy(reinterpret_cast<uint32_t*>(gconf), reinterpret_cast<const uint32_t*>(t.colconf), c.ncol);
+    for (int i = threadIdx.x; i < HTM_MAXPAT * HTM_MAXACT; i += TM_NT) {
+        gpat[i] = (&sh->inf_pat[0][0])[i];
+        gpat[HTM_MAXPAT * HTM_MAXACT + i] = (&sh->lrn_pat[0][0])[i];
+    }
+    if (threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
+    if (threadIdx.x < HTM_MAXPAT) {
+        hdr->inf_pat_len[threadIdx.x] = sh->inf_len[threadIdx.x];
+        hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
+    }
+    if (threadIdx.x == 0) {
+        hdr->avg_input_density = sh->avg_dens;
+        hdr->avg_learned_seq_length = sh->avg_lsl;
+        hdr->lrn_iter = sh->lrn_iter;
+        hdr->iter = sh->iter;
+        hdr->pam_counter = sh->pam;
+        hdr->learned_seq_length = sh->lsl;
+        hdr->reset_called = 0;
+        hdr->have_avg_density = sh->have_avg;
+        hdr->rng_f = sh->rf;
+        hdr->rng_r = sh->rr;
+        hdr->seg_hwm = sh->hwm;
+        hdr->seg_live = sh->nlive;
+        hdr->n_inf_pat = sh->n_inf_pat;
+        hdr->n_lrn_pat = sh->n_lrn_pat;
+        hdr->inf_pat_head = (uint16_t)sh->inf_head;
+        hdr->lrn_pat_head = (uint16_t)sh->lrn_head;
+        hdr->n_upd = sh->n_upd;
+        hdr->error = sh->err;
+        hdr->stat_inf_phase2 = sh->st[0];
+        hdr->stat_inf_backtrack = sh->st[1];
+        hdr->stat_lrn_phase2 = sh->st[2];
+        hdr->stat_lrn_backtrack = sh->st[3];
+    }
+}
+
+int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen, int n,
+                   hipStream_t st) {
+    size_t lds = tm_step_lds_bytes(c, learn, frozen);
+    if (learn) {
+        hipLaunchKernelGGL((tm_step_kernel<true, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, scores, 0);
+    } else if (frozen) {
+        hipLaunchKernelGGL((tm_step_kernel<false, true>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, scores, 0);
+    } else {
+        hipLaunchKernelGGL((tm_step_kernel<false, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, scores, 0);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// init / reset
+__global__ void tm_init_kernel(DevCfg c, TmBufs b, const uint64_t* seeds, int n) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    htm_tm_header* h = b.hdr + s;
+    uint32_t st[31];
+    int32_t f, r;
+    rng_seed(st, f, r, seeds[s]);
+    for (int i = 0; i < 31; i++) h->rng_state[i] = st[i];
+    h->rng_f = f;
+    h->rng_r = r;
+    h->pam_counter = c.pam_len;
+}
+
+int launch_tm_init(const DevCfg& c, const TmBufs& b, const uint64_t* seeds, int n, hipStream_t st) {
+    hipLaunchKernelGGL(tm_init_kernel, dim3((n + 63) / 64), dim3(64), 0, st, c, b, seeds, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// BacktrackingTM.reset(): clears t and t-1 states (colConfidence is kept),
+// flushes the update queue and the pattern histories
+__global__ void tm_reset_kernel(DevCfg c, TmBufs b) {
+    int s = blockIdx.x;
+    uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
+    for (int i = threadIdx.x; i < 4 * c.cw; i += blockDim.x) gbm[i] = 0u;
+    if (threadIdx.x == 0) {
+        htm_tm_header* h = b.hdr + s;
+        h->n_upd = 0;
+        h->reset_called = 1;
+        h->n_inf_pat = 0;
+        h->n_lrn_pat = 0;
+    }
+}
+
+int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+    hipLaunchKernelGGL(tm_reset_kernel, dim3(n), dim3(256), 0, st, c, b);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// Frozen forward index build.  counts[s] = total entries of stream s.
+// fx_off[s] doubles as the per-(cell, window) counter array.
+__global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
+    const int s = blockIdx.x;
+    const size_t sc = (size_t)c.seg_cap;
+    const uint32_t* meta = b.seg_meta + (size_t)s * sc;
+    const uint16_t* src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
+    const size_t noff = (size_t)c.ncells * c.fx_nwin + 1;
+    uint32_t* off = b.fx_off + (size_t)s * noff;
+    const uint32_t hwm = b.hdr[s].seg_hwm;
+    for (size_t i = threadIdx.x; i < noff; i += blockDim.x) off[i] = 0u;
+    __syncthreads();
+    for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
+        uint32_t m = meta[slot];
+        if (!meta_live(m)) continue;
+        uint32_t nsyn = meta_nsyn(m), w = slot / (uint32_t)c.fx_win;
+        for (uint32_t j = 0; j < nsyn; j++) atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+    }
+    __syncthreads();
+    // exclusive scan over noff entries (chunked per thread)
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t tot;
+    const size_t per = (noff + blockDim.x - 1) / blockDim.x;
+    const size_t i0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (size_t k = 0; k < per && i0 + k < noff; k++) sum += off[i0 + k];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < (int)blockDim.x; k++) { uint32_t v = part[k]; part[k] = run; run += v; }
+        tot = run;
+    }
+    __syncthreads();
+    uint32_t run = part[threadIdx.x];
+    for (size_t k = 0; k < per && i0 + k < noff; k++) {
+        uint32_t v = off[i0 + k];
+        off[i0 + k] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) counts[s] = tot;
+}
+
+int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st) {
+    hipLaunchKernelGGL(tm_fx_count_kernel, dim3(n), dim3(256), 0, st, c, b, counts);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// fill: per-(cell, window) cursors in scr_cur
+__global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
+    const int s = blockIdx.x;
+    const size_t sc = (size_t)c.seg_cap;
+    const uint32_t* meta = b.seg_meta + (size_t)s * sc;
+    const uint16_t* src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
+    const size_t noff = (size_t)c.ncells * c.fx_nwin + 1;
+    const uint32_t* off = b.fx_off + (size_t)s * noff;
+    uint32_t* cur = b.scr_cur + (size_t)s * ((size_t)c.ncells * c.fx_nwin);
+    uint32_t* ent = b.fx_ent + b.fx_base[s];
+    const uint32_t hwm = b.hdr[s].seg_hwm;
+    for (size_t i = threadIdx.x; i + 1 < noff; i += blockDim.x) cur[i] = off[i];
+    __syncthreads();
+    for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
+        uint32_t m = meta[slot];
+        if (!meta_live(m)) continue;
+        uint32_t nsyn = meta_nsyn(m), w = slot / (uint32_t)c.fx_win;
+        for (uint32_t j = 0; j < nsyn; j++) {
+            uint32_t pos = atomicAdd(&cur[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+            ent[pos] = slot;
+        }
+    }
+}
+
+int tm_configure_lds(const DevCfg& c) {
+    // the frozen variant may exceed the default 64 KiB dynamic LDS limit
+    size_t b0 = tm_step_lds_bytes(c, 1, 0), b1 = tm_step_lds_bytes(c, 0, 1), b2 = tm_step_lds_bytes(c, 0, 0);
+    hipError_t e0 = hipFuncSetAttribute((const void*)tm_step_kernel<true, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b0);
+    hipError_t e1 = hipFuncSetAttribute((const void*)tm_step_kernel<false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
+    hipError_t e2 = hipFuncSetAttribute((const void*)tm_step_kernel<false, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
+    (void)hipGetLastError();
+    return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess) ? 0 : -1;
+}
+
+int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+    hipLaunchKernelGGL(tm_fx_fill_kernel, dim3(n), dim3(256), 0, st, c, b);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

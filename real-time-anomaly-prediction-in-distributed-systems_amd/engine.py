@@ -1,0 +1,251 @@
+"""Batched HTM engine: N Model-1 streams stepped in lockstep on one MI355X.
+
+Thin Python owner of a `htm_engine*` (include/htm_amd.h).  Device buffers for
+inputs/scores are torch tensors (PyTorch-ROCm is the plumbing); every
+computation runs in the HIP kernels of libhtm_amd.so.
+
+Reference: one NuPIC `Network` per stream, driven by
+ML/HTM/NetworkModel.py:35-157 (runNetwork/run) from ModelTraining.py /
+ModelTesting.py; this engine replaces that per-stream loop.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import OUT, ST, HtmConfig, TmHeader, TmUpdate, check
+
+
+class HTMEngine:
+    """N independent encoder->SP->TM->anomaly streams on one GPU.
+
+    >>> eng = HTMEngine(1024)                       # reference Model-1 params
+    >>> scores = eng.step(torch.full((1024,), 42.0, device="cuda", dtype=torch.float64))
+    """
+
+    def __init__(self, n_streams: int, config: HtmConfig | None = None, device: int | None = None,
+                 _handle=None, **overrides):
+        self._L = _lib.lib()
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        if _handle is not None:
+            self.h = _handle
+        else:
+            cfg = config if config is not None else _lib.default_config(**overrides)
+            h = ctypes.c_void_p()
+            with torch.cuda.device(self.device):
+                check(self._L.htm_create(ctypes.byref(cfg), int(n_streams), self.device, ctypes.byref(h)))
+            self.h = h
+        cfg = HtmConfig()
+        check(self._L.htm_get_config(self.h, ctypes.byref(cfg)))
+        self.config = cfg
+        self.n_streams = self._L.htm_n_streams(self.h)
+        self.n_fields = cfg.n_fields
+        self.n_columns = cfg.sp_columns
+        self.cells_per_column = cfg.tm_cells_per_col
+        self.n_cells = cfg.sp_columns * cfg.tm_cells_per_col
+        self.sp_learn = True
+        self.tm_learn = True
+
+    # ------------------------------------------------------------------ life
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.htm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------- controls
+    def set_learning(self, sp: bool, tm: bool):
+        """SPRegion / TMRegion setParameter('learningMode', ...) (independent)."""
+        check(self._L.htm_set_learning(self.h, int(bool(sp)), int(bool(tm))))
+        self.sp_learn, self.tm_learn = bool(sp), bool(tm)
+
+    def set_option(self, opt: int, value: int):
+        check(self._L.htm_set_option(self.h, int(opt), int(value)))
+
+    def use_frozen_index(self, on: bool):
+        self.set_option(_lib.OPT_FROZEN_INDEX, int(on))
+
+    def keep_prev_predicted(self, on: bool):
+        self.set_option(_lib.OPT_KEEP_PREV, int(on))
+
+    def tm_reset(self):
+        check(self._L.htm_reset_tm(self.h, self._stream()))
+
+    def status(self):
+        """Synchronise and raise on any per-stream capacity overflow."""
+        check(self._L.htm_status(self.h))
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ----------------------------------------------------------------- steps
+    def _values(self, values) -> torch.Tensor:
+        if not isinstance(values, torch.Tensor):
+            values = torch.as_tensor(np.asarray(values, dtype=np.float64))
+        v = values.to(device=f"cuda:{self.device}", dtype=torch.float64).contiguous()
+        return v
+
+    def step(self, values, out: torch.Tensor | None = None) -> torch.Tensor:
+        """One network.run(1) for every stream; returns float32 anomaly scores [N]."""
+        v = self._values(values)
+        if v.numel() != self.n_streams * self.n_fields:
+            raise ValueError(f"expected {self.n_streams * self.n_fields} values, got {v.numel()}")
+        if out is None:
+            out = torch.empty(self.n_streams, dtype=torch.float32, device=v.device)
+        check(self._L.htm_step(self.h, ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                               self._stream()))
+        return out
+
+    def run(self, values, out: torch.Tensor | None = None) -> torch.Tensor:
+        """values [T, N(, F)] -> scores [T, N]."""
+        v = self._values(values)
+        T = v.shape[0]
+        if v.numel() != T * self.n_streams * self.n_fields:
+            raise ValueError("values must be [T, n_streams(, n_fields)]")
+        if out is None:
+            out = torch.empty((T, self.n_streams), dtype=torch.float32, device=v.device)
+        check(self._L.htm_run(self.h, T, ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                              self._stream()))
+        return out
+
+    # --------------------------------------------------------------- outputs
+    def get_output(self, name: str) -> torch.Tensor:
+        """region.getOutputData(...) for every stream (device tensor)."""
+        which = OUT[name]
+        per = self._L.htm_output_bytes(self.h, which)
+        dtype = {"active_columns": torch.uint8, "prev_pred_columns": torch.uint8,
+                 "col_confidence": torch.float32, "sp_overlaps": torch.int32}.get(name, torch.int32)
+        esz = torch.tensor([], dtype=dtype).element_size()
+        out = torch.empty((self.n_streams, per // esz), dtype=dtype, device=f"cuda:{self.device}")
+        check(self._L.htm_get_output(self.h, which, ctypes.c_void_p(out.data_ptr()), per * self.n_streams,
+                                     self._stream()))
+        return out
+
+    def bitmap_to_dense(self, words: torch.Tensor) -> np.ndarray:
+        """uint32 cell bitmaps [N, cells/32] -> uint8 [N, cells]."""
+        w = words.detach().cpu().numpy().astype(np.uint32).view(np.uint8)
+        bits = np.unpackbits(w.reshape(w.shape[0], -1), axis=1, bitorder="little")
+        return bits[:, : self.n_cells]
+
+    # ----------------------------------------------------------------- state
+    def state_bytes(self, region: str) -> int:
+        return self._L.htm_state_bytes(self.h, ST[region])
+
+    def export_state(self, region: str, s0: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.n_streams - s0 if n is None else n
+        per = self.state_bytes(region)
+        buf = np.zeros(per * n, np.uint8)
+        check(self._L.htm_export_state(self.h, ST[region], s0, n, buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes))
+        return buf.reshape(n, per)
+
+    def import_state(self, region: str, data: np.ndarray, s0: int = 0):
+        data = np.ascontiguousarray(data)
+        per = self.state_bytes(region)
+        n = data.nbytes // per
+        check(self._L.htm_import_state(self.h, ST[region], s0, n, data.ctypes.data_as(ctypes.c_void_p), data.nbytes))
+
+    def tm_header(self, s: int) -> TmHeader:
+        raw = self.export_state("tm_header", s, 1)[0]
+        return TmHeader.from_buffer_copy(raw.tobytes())
+
+    def replicate(self, src: int = 0):
+        """Copy stream `src` into every stream (config-2 setup)."""
+        check(self._L.htm_replicate_stream(self.h, int(src), self._stream()))
+
+    def device_bytes(self) -> int:
+        return self._L.htm_device_bytes(self.h)
+
+    def frozen_index_valid(self) -> bool:
+        return bool(self._L.htm_frozen_index_valid(self.h))
+
+    # -------------------------------------------------------------- save/load
+    def save(self, path: str):
+        check(self._L.htm_save(self.h, path.encode()))
+
+    @classmethod
+    def load(cls, path: str, device: int | None = None) -> "HTMEngine":
+        L = _lib.lib()
+        dev = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(L.htm_load(path.encode(), dev, ctypes.byref(h)))
+        return cls(0, device=dev, _handle=h)
+
+    # ------------------------------------------------- canonical state views
+    def sp_state(self, s: int) -> dict:
+        """SP state of stream s in the oracle's dense layout."""
+        c = self.config
+        nin = c.n_fields * c.enc_n
+        nin_pad = (nin + 31) // 32 * 32
+        nw = c.sp_columns // 32
+        pot_words = self.export_state("sp_potmask", s, 1)[0].view(np.uint32).reshape(c.sp_columns, nin_pad // 32)
+        pot = np.unpackbits(pot_words.view(np.uint8).reshape(c.sp_columns, -1), axis=1, bitorder="little")[:, :nin]
+        packed = self.export_state("sp_perm", s, 1)[0].view(np.float32).reshape(c.sp_columns, -1)
+        perm = np.zeros((c.sp_columns, nin), np.float32)
+        for col in range(c.sp_columns):
+            idx = np.nonzero(pot[col])[0]
+            perm[col, idx] = packed[col, : len(idx)]
+        connT = self.export_state("sp_connT", s, 1)[0].view(np.uint32).reshape(nin_pad, nw)
+        conn = np.unpackbits(connT.view(np.uint8).reshape(nin_pad, -1), axis=1, bitorder="little")[:nin, :c.sp_columns]
+        duty = self.export_state("sp_duty", s, 1)[0].view(np.float32).reshape(2, c.sp_columns)
+        sc = self.export_state("sp_scalars", s, 1)[0].view(np.uint32)
+        return dict(perm=perm, potential=pot.astype(np.uint8), connected=conn.T.copy().astype(np.uint8),
+                    overlap_dc=duty[0].copy(), active_dc=duty[1].copy(),
+                    min_overlap_dc=np.float32(sc[2:3].view(np.float32)[0]), iter=int(sc[0]), iter_learn=int(sc[1]))
+
+    def tm_segments(self, s: int) -> dict:
+        """Live segments of stream s in canonical (cell, creation) order, the
+        layout of oracle.OracleModel.tm_segments(32)."""
+        meta = self.export_state("tm_seg_meta", s, 1)[0].view(np.uint32)
+        hdr = self.tm_header(s)
+        hwm = hdr.seg_hwm
+        meta = meta[:hwm]
+        live = ((meta >> 23) & 1).astype(bool)
+        slots = np.nonzero(live)[0]
+        cell = (meta[slots] & 0xFFFF).astype(np.int64)
+        order = np.lexsort((slots, cell))
+        slots = slots[order]
+        m = meta[slots]
+        src = self.export_state("tm_seg_src", s, 1)[0].view(np.uint16).reshape(-1, 32)[slots].astype(np.int32)
+        perm = self.export_state("tm_seg_perm", s, 1)[0].view(np.float32).reshape(-1, 32)[slots]
+        duty = self.export_state("tm_seg_duty", s, 1)[0].view(np.uint32).reshape(-1, 3)[slots]
+        nsyn = ((m >> 16) & 0x3F).astype(np.int32)
+        mask = np.arange(32)[None, :] < nsyn[:, None]
+        return dict(cell=(m & 0xFFFF).astype(np.int32), is_seq=((m >> 22) & 1).astype(np.int32),
+                    pos_act=duty[:, 0].astype(np.int32), last_dc_iter=duty[:, 2].astype(np.int32), nsyn=nsyn,
+                    last_dc=duty[:, 1].copy().view(np.float32), src=np.where(mask, src, 0),
+                    perm=np.where(mask, perm, np.float32(0)), slots=slots)
+
+    def tm_states(self, s: int) -> dict:
+        c = self.config
+        cw = self.n_cells // 32
+        bm = self.export_state("tm_bitmaps", s, 1)[0].view(np.uint32).reshape(4, cw)
+        dense = np.unpackbits(bm.view(np.uint8).reshape(4, -1), axis=1, bitorder="little")[:, : self.n_cells]
+        return dict(inf_active=dense[0], inf_pred=dense[1], lrn_active=dense[2], lrn_pred=dense[3])
+
+    def col_confidence(self, s: int) -> np.ndarray:
+        return self.export_state("tm_colconf", s, 1)[0].view(np.float32).copy()
+
+    def tm_patterns(self, s: int) -> tuple[list, list]:
+        hdr = self.tm_header(s)
+        pat = self.export_state("tm_patterns", s, 1)[0].view(np.uint16).reshape(2, 16, 64)
+        inf = [pat[0][(hdr.inf_pat_head + k) % 16][: hdr.inf_pat_len[(hdr.inf_pat_head + k) % 16]].tolist()
+               for k in range(hdr.n_inf_pat)]
+        lrn = [pat[1][(hdr.lrn_pat_head + k) % 16][: hdr.lrn_pat_len[(hdr.lrn_pat_head + k) % 16]].tolist()
+               for k in range(hdr.n_lrn_pat)]
+        return inf, lrn
+
+    def tm_updates(self, s: int) -> list:
+        hdr = self.tm_header(s)
+        raw = self.export_state("tm_updates", s, 1)[0]
+        n = hdr.n_upd
+        arr = (TmUpdate * (len(raw) // ctypes.sizeof(TmUpdate))).from_buffer_copy(raw.tobytes())
+        return [arr[k] for k in range(n)]
