@@ -116,7 +116,18 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                   frozen cell->segment forward index; 0: scan the pool */
 #define HTM_OPT_KEEP_PREV 2    /* 1: retain prevPredictedColumns for HTM_OUT_PREV_PRED_COLS */
 #define HTM_OPT_KEEP_OVERLAPS 3 /* 1: retain SP overlaps for HTM_OUT_SP_OVERLAPS */
+#define HTM_OPT_PROFILE 4       /* 1: bracket each step's SP and TM kernels with HIP events */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
+
+/* Kernel times of the profiled steps since the last call (synchronises):
+ * out4 = {SP kernel ms, TM kernel ms, profiled steps, 0}. */
+int htm_profile_read(htm_engine* eng, double* out4);
+
+/* Sum over streams of the TM counters (synchronises): out8 = {algorithmic HBM
+ * bytes moved by the TM kernel, inferPhase2 calls, inferBacktracks,
+ * learnPhase2 calls, learnBacktracks, live segments, pool high-water marks,
+ * OR of error flags}. */
+int htm_counters(htm_engine* eng, uint64_t* out8);
 
 /* Synchronise and check every stream's overflow flags (HTM_E_CAPACITY). */
 int htm_status(htm_engine* eng);
@@ -187,6 +198,7 @@ typedef struct {
     uint32_t stat_inf_phase2, stat_inf_backtrack, stat_lrn_phase2, stat_lrn_backtrack;
     uint16_t inf_pat_head, lrn_pat_head; /* ring-buffer heads of the histories */
     uint32_t pad;
+    uint64_t stat_bytes;     /* algorithmic HBM bytes moved by the TM kernel (accumulated) */
 } htm_tm_header;
 
 /* A queued segment update (BacktrackingTM segmentUpdates entry). */

@@ -28,6 +28,7 @@ ST = dict(sp_connT=1, sp_potmask=2, sp_perm=3, sp_duty=4, sp_scalars=5, tm_heade
 OPT_FROZEN_INDEX = 1
 OPT_KEEP_PREV = 2
 OPT_KEEP_OVERLAPS = 3
+OPT_PROFILE = 4
 
 
 class HtmConfig(ctypes.Structure):
@@ -71,6 +72,7 @@ class TmHeader(ctypes.Structure):
         ("stat_inf_phase2", ctypes.c_uint32), ("stat_inf_backtrack", ctypes.c_uint32),
         ("stat_lrn_phase2", ctypes.c_uint32), ("stat_lrn_backtrack", ctypes.c_uint32),
         ("inf_pat_head", ctypes.c_uint16), ("lrn_pat_head", ctypes.c_uint16), ("pad", ctypes.c_uint32),
+        ("stat_bytes", ctypes.c_uint64),
     ]
 
 
@@ -86,6 +88,7 @@ EXPORTED = [
     "htm_step", "htm_run", "htm_get_output", "htm_output_bytes", "htm_state_bytes", "htm_export_state",
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
+    "htm_profile_read", "htm_counters",
 ]
 
 _lib = None
@@ -148,6 +151,8 @@ def lib():
     L.htm_frozen_index_valid.restype = i32
     L.htm_last_error.restype = ctypes.c_char_p
     L.htm_abi_version.restype = i32
+    L.htm_profile_read.argtypes = [vp, P(ctypes.c_double)]
+    L.htm_counters.argtypes = [vp, P(ctypes.c_uint64)]
     _lib = L
     return L
 

@@ -63,6 +63,9 @@ struct htm_engine {
     size_t fx_cap = 0;
     uint64_t* d_counts = nullptr;
     Region regions[17];
+    int32_t profile = 0;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
 };
 
 extern "C" {
@@ -356,6 +359,7 @@ int htm_destroy(htm_engine* e) {
     hipDeviceSynchronize();
     for (void* p : e->allocs) hipFree(p);
     if (e->tm.fx_ent) hipFree(e->tm.fx_ent);
+    for (hipEvent_t x : e->ev_pool) (void)hipEventDestroy(x);
     delete e;
     return HTM_OK;
 }
@@ -373,6 +377,10 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
     if (opt == HTM_OPT_FROZEN_INDEX) e->use_frozen = value ? 1 : 0;
     else if (opt == HTM_OPT_KEEP_PREV) e->keep_prev = value ? 1 : 0;
     else if (opt == HTM_OPT_KEEP_OVERLAPS) e->keep_overlaps = value ? 1 : 0;
+    else if (opt == HTM_OPT_PROFILE) {
+        e->profile = value ? 1 : 0;
+        e->ev_used = 0;
+    }
     else return fail(HTM_E_INVALID, "unknown option %d", opt);
     return HTM_OK;
 }
@@ -408,10 +416,21 @@ static int build_fx(htm_engine* e, hipStream_t st) {
 
 extern "C" {
 
+static int next_events(htm_engine* e, hipEvent_t* ev) {
+    // three events per profiled step: before SP, between SP and TM, after TM
+    while (e->ev_pool.size() < e->ev_used + 3) {
+        hipEvent_t x;
+        HIP_TRY(hipEventCreate(&x));
+        e->ev_pool.push_back(x);
+    }
+    for (int k = 0; k < 3; k++) ev[k] = e->ev_pool[e->ev_used + k];
+    e->ev_used += 3;
+    return HTM_OK;
+}
+
 int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
     if (!e || !d_values || !d_scores) return fail(HTM_E_INVALID, "bad arguments");
     hipStream_t st = (hipStream_t)stream;
-    if (launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st)) return fail(HTM_E_HIP, "sp_step launch");
     int frozen = 0;
     if (e->tm_learn) {
         e->fx_valid = false;
@@ -422,12 +441,65 @@ int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* strea
         }
         frozen = 1;
     }
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (e->profile) {
+        int r = next_events(e, ev);
+        if (r) return r;
+        HIP_TRY(hipEventRecord(ev[0], st));
+    }
+    if (launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st))
+        return fail(HTM_E_HIP, "sp_step launch");
     if (e->keep_prev) {
         // prevPredictedColumns (nonzero colConfidence before compute)
         if (launch_prev_pred(e->dc, e->tm, e->n, st)) return fail(HTM_E_HIP, "prev_pred launch");
     }
+    if (e->profile) HIP_TRY(hipEventRecord(ev[1], st));
     if (launch_tm_step(e->dc, e->tm, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
         return fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
+    if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
+    return HTM_OK;
+}
+
+// Kernel times of the profiled steps since the last read:
+// out4 = {SP kernel ms, TM kernel ms, steps, 0}
+int htm_profile_read(htm_engine* e, double* out4) {
+    if (!e || !out4) return fail(HTM_E_INVALID, "bad arguments");
+    HIP_TRY(hipDeviceSynchronize());
+    double sp = 0.0, tm = 0.0;
+    for (size_t k = 0; k + 2 < e->ev_used + 1 && k < e->ev_used; k += 3) {
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, e->ev_pool[k], e->ev_pool[k + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, e->ev_pool[k + 1], e->ev_pool[k + 2]));
+        sp += a;
+        tm += b;
+    }
+    out4[0] = sp;
+    out4[1] = tm;
+    out4[2] = (double)(e->ev_used / 3);
+    out4[3] = 0.0;
+    e->ev_used = 0;
+    return HTM_OK;
+}
+
+// Sum of the per-stream TM counters: out8 = {algorithmic bytes, inferPhase2
+// calls, inferBacktracks, learnPhase2 calls, learnBacktracks, live segments,
+// pool high-water marks, OR of error flags}
+int htm_counters(htm_engine* e, uint64_t* out8) {
+    if (!e || !out8) return fail(HTM_E_INVALID, "bad arguments");
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<htm_tm_header> h((size_t)e->n);
+    HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 8; k++) out8[k] = 0;
+    for (const auto& x : h) {
+        out8[0] += x.stat_bytes;
+        out8[1] += x.stat_inf_phase2;
+        out8[2] += x.stat_inf_backtrack;
+        out8[3] += x.stat_lrn_phase2;
+        out8[4] += x.stat_lrn_backtrack;
+        out8[5] += x.seg_live;
+        out8[6] += x.seg_hwm;
+        out8[7] |= x.error;
+    }
     return HTM_OK;
 }
 

@@ -36,6 +36,8 @@ __constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 10000
 
 struct __attribute__((aligned(16))) TmSh {
     double avg_dens, avg_lsl;
+    unsigned long long bytes;  // algorithmic HBM bytes of this step (thread 0 / LDS atomics)
+    uint32_t ecount;           // frozen-index entries read by one collection
     uint32_t lrn_iter, iter;
     int32_t pam, lsl, reset, have_avg;
     uint32_t rng[31];
@@ -245,13 +247,16 @@ __device__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start
 __device__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
     const uint32_t hwm = t.sh->hwm;
     const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    uint32_t nb = 0;  // bytes read by this thread
     for (uint32_t base = 0; base < hwm; base += TM_NT / 4) {
         uint32_t slot = base + g;
         uint32_t m = slot < hwm ? t.meta[slot] : 0u;
+        if (slot < hwm && sub == 0) nb += 4;
         uint32_t nsyn = meta_nsyn(m);
         bool live = meta_live(m);
         uint32_t mask = 0;
         if (live && (uint32_t)(sub * 8) < nsyn) {
+            nb += 16;
             uint4 v = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
             uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -268,6 +273,8 @@ __device__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
             t.q1[i] = slot;
         }
     }
+    nb = wg_sum(t.sh, nb);
+    if (threadIdx.x == 0) t.sh->bytes += nb;
 }
 
 // learning-off form: forward propagation over the frozen cell->segment index
@@ -279,12 +286,14 @@ __device__ void collect_frozen(Tm& t, int thr) {
     const uint32_t ncells_act = nact < 2048 ? nact : 2048;
     const uint32_t hwm = t.sh->hwm;
     const uint32_t W = (uint32_t)c.fx_win;
+    if (threadIdx.x == 0) t.sh->ecount = 0;
     for (uint32_t w = 0; w * W < hwm; w++) {
         wg_clear(cnt, (int)(W / 4));
         __syncthreads();
         for (uint32_t k = wave_id(); k < ncells_act; k += TM_NWAVES) {
             const uint32_t* o = t.fxoff + (size_t)cells[k] * c.fx_nwin + w;
             uint32_t lo = o[0], hi = o[1];
+            if (lane_id() == 0) atomicAdd(&t.sh->ecount, hi - lo + 2u);  // entries + the two offsets
             for (uint32_t e = lo + lane_id(); e < hi; e += 64) {
                 uint32_t rel = t.fxent[e] - w * W;
                 atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
@@ -304,6 +313,7 @@ __device__ void collect_frozen(Tm& t, int thr) {
         }
         __syncthreads();
     }
+    if (threadIdx.x == 0) t.sh->bytes += 4ull * t.sh->ecount;
 }
 
 // Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
@@ -319,10 +329,13 @@ __device__ uint32_t phase2_finish(Tm& t) {
     wg_clear(colcnt, c.ncol);
     __syncthreads();
     // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
+    uint32_t nb = 0;
     for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
         uint32_t slot = t.q1[k];
         uint32_t m = t.meta[slot];
         uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
+        // meta + conn + used source rows + duty-cycle record read and written
+        nb += 4u + 4u + 16u * ((nsyn + 7u) / 8u) + 12u + 8u;
         uint32_t cm = t.conn[slot];
         const uint4* row = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
         uint32_t n = 0;
@@ -341,7 +354,8 @@ __device__ uint32_t phase2_finish(Tm& t) {
         (void)seg_dc_update(t.duty, slot, sh->lrn_iter, false);
         atomicAdd(&colcnt[col_of(c, cell)], 1u);
     }
-    __syncthreads();
+    nb = wg_sum(sh, nb);
+    if (threadIdx.x == 0) sh->bytes += nb;
     // exclusive scan of bucket counts + nonzero column list (ascending)
     const int per = (c.ncol + TM_NT - 1) / TM_NT;
     const int c0 = threadIdx.x * per;
@@ -496,6 +510,10 @@ __device__ void infer_backtrack(Tm& t) {
         }
         sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
         sh->n_inf_pat -= npop;
+        // scratch traffic: backup out + in, candidate out + in
+        unsigned long long bb = 2ull * 4ull * cw + 4ull * cw + (haveCand ? 0ull : 4ull * cw);
+        if (haveCand && candStart != cur) bb += 2ull * (2ull * 4ull * cw + 4ull * t.c.ncol);
+        sh->bytes += bb;
     }
     wg_copy(t.infP1, bkP, cw);
     __syncthreads();
@@ -543,14 +561,17 @@ __device__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t*
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
     const uint32_t hwm = t.sh->hwm;
     const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    uint32_t nb = 0;
     for (uint32_t base = 0; base < hwm; base += TM_NT / 4) {
         uint32_t slot = base + g;
         uint32_t m = slot < hwm ? t.meta[slot] : 0u;
+        if (slot < hwm && sub == 0) nb += 4;
         uint32_t nsyn = meta_nsyn(m), cell = meta_cell(m);
         uint32_t col = col_of(c, cell);
         bool elig = meta_live(m) && (!colflags || ((colflags[col >> 5] >> (col & 31)) & 1u));
         uint32_t mask = 0;
         if (elig && (uint32_t)(sub * 8) < nsyn) {
+            nb += 16;
             uint4 v = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
             uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -570,6 +591,8 @@ __device__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t*
             atomicMax(&keys[col], key);
         }
     }
+    nb = wg_sum(t.sh, nb);
+    if (threadIdx.x == 0) t.sh->bytes += nb;
 }
 
 __device__ __forceinline__ uint32_t key_slot(unsigned long long k) { return 0xFFFFFFFFu - (uint32_t)k; }
@@ -596,6 +619,7 @@ __device__ WUpd w_build_update(Tm& t, uint32_t slot, const uint32_t* state, bool
     u.mask = (uint32_t)__ballot(act);
     u.n_new = 0;
     u.my_new = 0;
+    if (l == 0 && exist) atomicAdd(&sh->bytes, (unsigned long long)(4 + 2 * nsyn));
     int n = want_new ? t.c.new_syn - __popc(u.mask) : 0;
     if (n <= 0) return u;
     const int ncand = sh->ncand;
@@ -660,6 +684,8 @@ __device__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t 
     if (l == 0) {
         t.duty[(size_t)slot * 3] += 1u;  // positiveActivations
         (void)seg_dc_update(t.duty, slot, t.sh->lrn_iter, true);
+        // meta, duty (r/w), sources + permanences (r/w), conn
+        atomicAdd(&t.sh->bytes, (unsigned long long)(4 + 24 + 2 * 6 * (nsyn + n_new) + 8));
     }
     const bool in = (uint32_t)l < nsyn;
     uint32_t sj = in ? srow[l] : 0u;
@@ -730,6 +756,7 @@ __device__ void w_trim_segment(Tm& t, uint32_t slot) {
     float p = in ? prow[l] : 0.0f;
     const bool del = in && p < 0.00001f;
     const uint32_t ndel = (uint32_t)__popcll(__ballot(del));
+    if (l == 0) atomicAdd(&t.sh->bytes, (unsigned long long)(4 + 6 * nsyn + (ndel ? 8 + 6 * (nsyn - ndel) : 0)));
     if (ndel == nsyn) {
         if (l == 0) {
             t.meta[slot] = m & ~(1u << 23);
@@ -778,6 +805,7 @@ __device__ void w_create_segment(Tm& t, uint32_t cell, uint32_t n_new, uint32_t 
         d[0] = 1u;
         d[1] = __float_as_uint((float)(1.0 / (double)sh->lrn_iter));
         d[2] = sh->lrn_iter;
+        atomicAdd(&sh->bytes, (unsigned long long)(4 + 4 + 12 + 6 * n_new + 1));
         t.nseg[cell] += 1;
         sh->hwm = slot + 1;
         sh->nlive += 1;
@@ -985,6 +1013,8 @@ __device__ void learn_phase2(Tm& t, bool ro) {
                     e.active_mask = u.mask;
                     e.date = sh->lrn_iter;
                     sh->n_upd = idx + 1;
+                    // queued entry written now and read back at the next step
+                    atomicAdd(&sh->bytes, (unsigned long long)(2 * (16 + 2 * u.n_new)));
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -1259,11 +1289,31 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
         sh->inf_len[threadIdx.x] = hdr->inf_pat_len[threadIdx.x];
         sh->lrn_len[threadIdx.x] = hdr->lrn_pat_len[threadIdx.x];
     }
-    for (int i = threadIdx.x; i < HTM_MAXPAT * HTM_MAXACT; i += TM_NT) {
-        (&sh->inf_pat[0][0])[i] = gpat[i];
-        (&sh->lrn_pat[0][0])[i] = gpat[HTM_MAXPAT * HTM_MAXACT + i];
-    }
     if (threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
+    __syncthreads();
+    // live pattern-history entries only (ring slots head .. head+n-1)
+    {
+        const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
+        for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
+            const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
+            if (k < ni) {
+                const int slot = (sh->inf_head + k) % HTM_MAXPAT;
+                if (a < sh->inf_len[slot]) sh->inf_pat[slot][a] = gpat[slot * HTM_MAXACT + a];
+            } else {
+                const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
+                if (a < sh->lrn_len[slot])
+                    sh->lrn_pat[slot][a] = gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a];
+            }
+        }
+        if (threadIdx.x == 0) {
+            unsigned long long pb = 0;
+            for (int k = 0; k < ni; k++) pb += 2ull * sh->inf_len[(sh->inf_head + k) % HTM_MAXPAT];
+            for (int k = 0; k < nl; k++) pb += 2ull * sh->lrn_len[(sh->lrn_head + k) % HTM_MAXPAT];
+            // header in/out, active list, bitmaps in (t-1), colConfidence in (active cols)
+            sh->bytes = pb + 2ull * sizeof(htm_tm_header) + 2ull * sh->nA + 4ull +
+                        (LEARN ? 3ull : 1ull) * 4ull * c.cw + 4ull * sh->nA;
+        }
+    }
     wg_copy(t.infP1, gbm + c.cw, c.cw);   // infPredictedState t -> t-1
     wg_copy(t.infP, gbm + c.cw, c.cw);
     if (LEARN) {
@@ -1307,9 +1357,17 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
         wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
     }
     wg_copy(reinterpret_cast<uint32_t*>(gconf), reinterpret_cast<const uint32_t*>(t.colconf), c.ncol);
-    for (int i = threadIdx.x; i < HTM_MAXPAT * HTM_MAXACT; i += TM_NT) {
-        gpat[i] = (&sh->inf_pat[0][0])[i];
-        gpat[HTM_MAXPAT * HTM_MAXACT + i] = (&sh->lrn_pat[0][0])[i];
+    // patterns only change by the push of this step (pops move the heads)
+    if (sh->ti[0] >= 0)
+        for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
+            gpat[sh->ti[0] * HTM_MAXACT + a] = sh->inf_pat[sh->ti[0]][a];
+    if (LEARN && sh->ti[1] >= 0)
+        for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
+            gpat[(HTM_MAXPAT + sh->ti[1]) * HTM_MAXACT + a] = sh->lrn_pat[sh->ti[1]][a];
+    if (threadIdx.x == 0) {
+        // bitmaps out, colConfidence out (dense), pushed patterns, score
+        sh->bytes += (LEARN ? 4ull : 2ull) * 4ull * c.cw + 4ull * c.ncol + (LEARN ? 4ull : 2ull) * sh->nA + 4ull;
+        hdr->stat_bytes += sh->bytes;
     }
     if (threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
     if (threadIdx.x < HTM_MAXPAT) {

@@ -163,6 +163,22 @@ class HTMEngine:
     def device_bytes(self) -> int:
         return self._L.htm_device_bytes(self.h)
 
+    def profile(self, on: bool):
+        """Bracket every step's SP and TM kernels with HIP events."""
+        self.set_option(_lib.OPT_PROFILE, int(on))
+
+    def profile_read(self) -> dict:
+        out = (ctypes.c_double * 4)()
+        check(self._L.htm_profile_read(self.h, out))
+        return dict(sp_ms=out[0], tm_ms=out[1], steps=int(out[2]))
+
+    def counters(self) -> dict:
+        out = (ctypes.c_uint64 * 8)()
+        check(self._L.htm_counters(self.h, out))
+        keys = ["tm_bytes", "inf_phase2", "inf_backtracks", "lrn_phase2", "lrn_backtracks", "seg_live",
+                "seg_hwm", "error"]
+        return {k: int(v) for k, v in zip(keys, out)}
+
     def frozen_index_valid(self) -> bool:
         return bool(self._L.htm_frozen_index_valid(self.h))
 
