@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -192,18 +193,19 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.seg_reserve = (c.tm_max_lrn_backtrack + 2) * c.sp_num_active;
     if (d.seg_reserve >= d.seg_cap) return fail(HTM_E_INVALID, "seg_capacity too small for one learning step");
     d.n_streams = n;
+    d.max_act_cells = d.num_desired * d.K;
+    d.q_lds = 1024;
     // frozen-inference counter window: the union region holds the u8
-    // counters (fx_win bytes) plus the active-cell list (4 KiB); fill the
-    // LDS budget so that two workgroups fit one CU
-    d.fx_win = 0;
-    d.fx_nwin = 1;
-    d.fx_win = 1024;  // provisional, to measure the rest of the layout
-    size_t off_u = tm_step_lds_bytes(d, 0, 1) - (size_t)(1024 / 4 + 1024) * 4;
-    size_t fin = ((size_t)d.ncol + (size_t)(d.ncol + 1) / 2 + (size_t)d.ncol + 1) * 4;
-    size_t win = lds_budget > off_u + 4096 ? lds_budget - off_u - 4096 : 0;
-    if (win < fin) win = fin;  // the union is at least the finish arrays anyway
+    // counters (fx_win bytes) plus the active-cell list and its block prefix;
+    // fill the LDS budget (two workgroups per CU by default).  Out-list
+    // entries are window-relative u16 with 0xFFFF as padding.
+    const size_t off_u = tm_step_lds_base(d, 0, 1);
+    const size_t cell_words = (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1;
+    size_t avail = lds_budget > off_u ? (lds_budget - off_u) / 4 : 0;
+    size_t win = avail > cell_words ? (avail - cell_words) * 4 : 0;
     win = (win / 1024) * 1024;
-    if (win < 4096) win = 4096;
+    if (win < 1024) win = 1024;
+    if (win > 64512) win = 64512;
     size_t capr = round_up((size_t)d.seg_cap, 1024);
     if (win > capr) win = capr;
     d.fx_win = (int32_t)win;
@@ -318,11 +320,18 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     e->device = device;
     int optin = query_lds_optin();
     size_t budget = optin >= 78 * 1024 ? (size_t)76 * 1024 : (size_t)optin - 2048;
+    if (const char* env = std::getenv("HTM_TM_LDS_BUDGET")) {  // tuning knob (bytes)
+        long v = std::strtol(env, nullptr, 10);
+        if (v >= 16384 && v <= optin) budget = (size_t)v;
+    }
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (!r) r = check_lds(e->dc);
     if (!r) r = allocate(e);
-    if (!r && tm_configure_lds(e->dc) && tm_step_lds_bytes(e->dc, 0, 1) > 65536)
-        r = fail(HTM_E_HIP, "cannot raise the dynamic LDS limit to %zu B", tm_step_lds_bytes(e->dc, 0, 1));
+    if (!r && tm_configure_lds(e->dc)) {
+        size_t mx = std::max(tm_step_lds_bytes(e->dc, 0, 1),
+                             std::max(tm_step_lds_bytes(e->dc, 1, 0), tm_step_lds_bytes(e->dc, 0, 0)));
+        if (mx > 65536) r = fail(HTM_E_HIP, "cannot raise the dynamic LDS limit to %zu B", mx);
+    }
     if (r) {
         for (void* p : e->allocs) hipFree(p);
         delete e;
@@ -400,13 +409,14 @@ static int build_fx(htm_engine* e, hipStream_t st) {
         tot += counts[s];
     }
     if (tot == 0) tot = 1;
-    if (tot > e->fx_cap) {
+    if (tot > e->fx_cap) {  // capacity in 16-byte blocks
         if (e->tm.fx_ent) HIP_TRY(hipFree(e->tm.fx_ent));
         e->tm.fx_ent = nullptr;
         size_t cap = (size_t)(tot + tot / 8 + 1024);
-        HIP_TRY(hipMalloc(&e->tm.fx_ent, cap * 4));
+        HIP_TRY(hipMalloc(&e->tm.fx_ent, cap * 16));
         e->fx_cap = cap;
     }
+    HIP_TRY(hipMemsetAsync(e->tm.fx_ent, 0xFF, (size_t)tot * 16, st));
     HIP_TRY(hipMemcpyAsync(e->tm.fx_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
     if (launch_tm_fx_fill(d, e->tm, e->n, st)) return fail(HTM_E_HIP, "fx fill launch");
     HIP_TRY(hipStreamSynchronize(st));
@@ -665,7 +675,7 @@ int htm_get_config(const htm_engine* e, htm_config* out) {
     return HTM_OK;
 }
 
-size_t htm_device_bytes(const htm_engine* e) { return e ? e->bytes + e->fx_cap * 4 : 0; }
+size_t htm_device_bytes(const htm_engine* e) { return e ? e->bytes + e->fx_cap * 16 : 0; }
 
 int32_t htm_frozen_index_valid(const htm_engine* e) { return e && e->fx_valid ? 1 : 0; }
 

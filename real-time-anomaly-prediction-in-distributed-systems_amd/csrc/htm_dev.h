@@ -41,8 +41,10 @@ struct DevCfg {
     int32_t min_thr, act_thr, pam_len, max_inf_bt, max_lrn_bt, max_seq_len, upd_valid;
     int32_t seg_cap, upd_cap;
     int32_t seg_reserve;                  // free slots needed before a learning step
-    int32_t fx_win;                       // frozen index: segments per LDS counter window
+    int32_t fx_win;                       // frozen index: segments per LDS counter window (<= 65536)
     int32_t fx_nwin;                      // windows covering seg_cap
+    int32_t q_lds;                        // qualifying segments sorted in LDS (more: global path)
+    int32_t max_act_cells;                // num_desired * K (frozen collection cell list)
     int32_t n_streams;
 };
 
@@ -79,11 +81,13 @@ struct TmBufs {
     uint8_t* prev_pred;     // [S][ncol] nonzero(colConf(t-1)) captured before compute
     uint32_t* scr_cur;      // [S][ncells*fx_nwin] frozen-index fill cursors
     // frozen forward index (valid while TM learning is off): for stream s,
-    // cell x and counter window w the segment slots with a synapse from x
-    // are fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1])
-    uint64_t* fx_base;      // [S]
-    uint32_t* fx_off;       // [S][ncells][fx_nwin] + 1 (running, stream relative)
-    uint32_t* fx_ent;       // [total] segment slots
+    // cell x and counter window w, the window-relative slots (u16) of the
+    // segments with a synapse from x fill the 16-byte blocks
+    // fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1]), padded
+    // with 0xFFFF, so one uint4 load delivers 8 entries of one list
+    uint64_t* fx_base;      // [S] first block of the stream
+    uint32_t* fx_off;       // [S][ncells][fx_nwin] + 1 (running block offsets)
+    uint4* fx_ent;          // [total blocks] 8 x u16 entries each
 };
 
 // ---------------------------------------------------------------------------
@@ -224,5 +228,6 @@ int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen);
+size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen);  // offset of the union region
 int tm_configure_lds(const DevCfg& c);
 int launch_prev_pred(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

@@ -37,7 +37,6 @@ __constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 10000
 struct __attribute__((aligned(16))) TmSh {
     double avg_dens, avg_lsl;
     unsigned long long bytes;  // algorithmic HBM bytes of this step (thread 0 / LDS atomics)
-    uint32_t ecount;           // frozen-index entries read by one collection
     uint32_t lrn_iter, iter;
     int32_t pam, lsl, reset, have_avg;
     uint32_t rng[31];
@@ -83,7 +82,7 @@ struct Tm {
     uint32_t* q1;
     uint32_t* q2;
     const uint32_t* fxoff;
-    const uint32_t* fxent;
+    const uint4* fxent;
 };
 
 // ---------------------------------------------------------------------------
@@ -107,11 +106,17 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     L.off_flags = o;
     o = align16(o + (size_t)c.nw * 4);
     L.off_U = o;
-    // union: finish (colcnt ncol + nzcol ncol/2 + nzstart ncol+1), keys (2 ncol),
-    // frozen collection (counters fx_win/4 + cell list 2048 u16), trim flags
-    size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1;
+    // union of phase-local arrays:
+    //  finish: colcnt[ncol] u32, nzcol[ncol] u16, nzstart[ncol+1] u32, and the
+    //          qualifying-segment buffers qkey/qdc/skey/sdc[q_lds]
+    //  keys (learning): best-match keys u64[ncol]
+    //  frozen collection: u8 counters[fx_win], active cells u16[max_act_cells],
+    //          block prefix u32[max_act_cells+1]
+    //  trim flags (learning): u32[upd_cap]
+    size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
+                 (size_t)(c.q_lds + 1) / 2;
     size_t keys = learn ? 2 * (size_t)c.ncol : 0;
-    size_t col = frozen ? (size_t)c.fx_win / 4 + 1024 : 0;
+    size_t col = frozen ? (size_t)c.fx_win / 4 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells + 1 : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
     size_t u = fin;
     if (keys > u) u = keys;
@@ -124,6 +129,7 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
 }
 
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).total; }
+size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).off_U; }
 
 // ---------------------------------------------------------------------------
 // workgroup helpers
@@ -277,26 +283,93 @@ __device__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
     if (threadIdx.x == 0) t.sh->bytes += nb;
 }
 
-// learning-off form: forward propagation over the frozen cell->segment index
+// one 16-byte block of a frozen out-list: 8 window-relative u16 slots,
+// 0xFFFF = padding; bump the slot's u8 counter
+__device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int h = 0; h < 8; h++) {
+        const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+        if (rel != 0xFFFFu) atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
+    }
+}
+
+// containing list of block b: k in [lo, hi) with pstart[k] <= b < pstart[k+1]
+__device__ __forceinline__ uint32_t fx_find(const uint32_t* pstart, uint32_t lo, uint32_t hi, uint32_t b) {
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pstart[mid] <= b) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// learning-off form: forward propagation over the frozen cell->segment index.
+// Per window of the slot space, the out-lists of the active cells are
+// concatenated (block prefix in LDS) and each wave streams a contiguous range
+// of that concatenation, 2 x 64 blocks (2 KB) in flight per wave, so the
+// loads are independent of list boundaries and of how skewed out-degrees are.
 __device__ void collect_frozen(Tm& t, int thr) {
     const DevCfg& c = t.c;
-    uint32_t* cnt = t.U;
-    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + c.fx_win / 4);
-    const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, 2048);
-    const uint32_t ncells_act = nact < 2048 ? nact : 2048;
-    const uint32_t hwm = t.sh->hwm;
+    TmSh* sh = t.sh;
     const uint32_t W = (uint32_t)c.fx_win;
-    if (threadIdx.x == 0) t.sh->ecount = 0;
+    const uint32_t mac = (uint32_t)c.max_act_cells;
+    uint32_t* cnt = t.U;
+    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4);
+    uint32_t* pstart = t.U + W / 4 + (mac + 1) / 2;
+    uint32_t* plo = pstart + mac + 1;
+    const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
+    const uint32_t na = nact < mac ? nact : mac;
+    const uint32_t hwm = sh->hwm;
+    const uint32_t nwin = (uint32_t)c.fx_nwin;
+    const uint32_t per = (na + TM_NT - 1) / TM_NT;
+    const uint32_t k0 = threadIdx.x * per;
+    const uint32_t lane = lane_id();
+    uint32_t nblk = 0;
     for (uint32_t w = 0; w * W < hwm; w++) {
+        uint32_t lsum = 0;
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t k = k0 + j;
+            if (k >= na) break;
+            const uint32_t* o = t.fxoff + (size_t)cells[k] * nwin + w;
+            const uint32_t lo = o[0], n = o[1] - lo;
+            plo[k] = lo;
+            pstart[k] = n;
+            lsum += n;
+        }
+        uint32_t B;
+        uint32_t pos = wg_excl_scan(sh, lsum, &B);
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t k = k0 + j;
+            if (k >= na) break;
+            const uint32_t n = pstart[k];
+            pstart[k] = pos;
+            pos += n;
+        }
+        if (threadIdx.x == 0) pstart[na] = B;
+        nblk += B;
         wg_clear(cnt, (int)(W / 4));
         __syncthreads();
-        for (uint32_t k = wave_id(); k < ncells_act; k += TM_NWAVES) {
-            const uint32_t* o = t.fxoff + (size_t)cells[k] * c.fx_nwin + w;
-            uint32_t lo = o[0], hi = o[1];
-            if (lane_id() == 0) atomicAdd(&t.sh->ecount, hi - lo + 2u);  // entries + the two offsets
-            for (uint32_t e = lo + lane_id(); e < hi; e += 64) {
-                uint32_t rel = t.fxent[e] - w * W;
-                atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
+        const uint32_t pw = (B + TM_NWAVES - 1) / TM_NWAVES;
+        const uint32_t b0 = wave_id() * pw;
+        const uint32_t b1 = b0 + pw < B ? b0 + pw : B;
+        if (b0 < b1) {
+            uint32_t kc = fx_find(pstart, 0, na, b0);
+            for (uint32_t base = b0; base < b1; base += 128) {
+                const uint32_t ba = base + lane, bb = base + 64 + lane;
+                const uint4 pad = make_uint4(~0u, ~0u, ~0u, ~0u);
+                uint4 va = pad, vb = pad;
+                uint32_t ka = kc, kb = kc;
+                if (ba < b1) {
+                    ka = fx_find(pstart, kc, na, ba);
+                    va = t.fxent[plo[ka] + (ba - pstart[ka])];
+                }
+                if (bb < b1) {
+                    kb = fx_find(pstart, ka, na, bb);
+                    vb = t.fxent[plo[kb] + (bb - pstart[kb])];
+                }
+                kc = wave_max_u32(kb > ka ? kb : ka);
+                fx_count_block(cnt, va);
+                fx_count_block(cnt, vb);
             }
         }
         __syncthreads();
@@ -313,7 +386,9 @@ __device__ void collect_frozen(Tm& t, int thr) {
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) t.sh->bytes += 4ull * t.sh->ecount;
+    // out-list blocks + the two block offsets of every (active cell, window)
+    const uint32_t nw = (hwm + W - 1) / W;
+    if (threadIdx.x == 0) sh->bytes += 16ull * nblk + 8ull * na * nw;
 }
 
 // Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
@@ -326,6 +401,15 @@ __device__ uint32_t phase2_finish(Tm& t) {
     uint32_t* colcnt = t.U;
     uint16_t* nzcol = reinterpret_cast<uint16_t*>(t.U + c.ncol);
     uint32_t* nzstart = t.U + c.ncol + (c.ncol + 1) / 2;
+    // qualifying segments (<= q_lds of them): key, dutyCycle, column; and
+    // the same sorted by column bucket
+    const uint32_t ql = (uint32_t)c.q_lds;
+    uint32_t* qkey = nzstart + c.ncol + 1;
+    float* qdc = reinterpret_cast<float*>(qkey + ql);
+    uint32_t* skey = qkey + 2 * ql;
+    float* sdc = reinterpret_cast<float*>(qkey + 3 * ql);
+    uint16_t* qcol = reinterpret_cast<uint16_t*>(qkey + 4 * ql);
+    const bool in_lds = qn <= ql;
     wg_clear(colcnt, c.ncol);
     __syncthreads();
     // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
@@ -351,8 +435,14 @@ __device__ uint32_t phase2_finish(Tm& t) {
             }
         }
         if (n >= (uint32_t)c.act_thr) atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
-        (void)seg_dc_update(t.duty, slot, sh->lrn_iter, false);
-        atomicAdd(&colcnt[col_of(c, cell)], 1u);
+        const float dc = seg_dc_update(t.duty, slot, sh->lrn_iter, false);
+        const uint32_t col = col_of(c, cell);
+        atomicAdd(&colcnt[col], 1u);
+        if (in_lds) {
+            qkey[k] = ((cell - col * K) << 27) | slot;
+            qdc[k] = dc;
+            qcol[k] = (uint16_t)col;
+        }
     }
     nb = wg_sum(sh, nb);
     if (threadIdx.x == 0) sh->bytes += nb;
@@ -382,37 +472,69 @@ __device__ uint32_t phase2_finish(Tm& t) {
     if (threadIdx.x == 0) nzstart[tnz] = tsum;
     __syncthreads();
     // pass 2: scatter keys (cellInColumn << 27 | slot) into column buckets
-    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
-        uint32_t slot = t.q1[k];
-        uint32_t cell = meta_cell(t.meta[slot]);
-        uint32_t col = col_of(c, cell);
-        uint32_t pos = atomicAdd(&colcnt[col], 1u);
-        t.q2[pos] = ((cell - col * K) << 27) | slot;
+    if (in_lds) {
+        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+            const uint32_t pos = atomicAdd(&colcnt[qcol[k]], 1u);
+            skey[pos] = qkey[k];
+            sdc[pos] = qdc[k];
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+            uint32_t slot = t.q1[k];
+            uint32_t cell = meta_cell(t.meta[slot]);
+            uint32_t col = col_of(c, cell);
+            uint32_t pos = atomicAdd(&colcnt[col], 1u);
+            t.q2[pos] = ((cell - col * K) << 27) | slot;
+        }
     }
     __syncthreads();
     // pass 3: per column, (cell, slot) order; float sum in that order
     uint32_t npcol = 0;
     for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) {
         uint32_t col = nzcol[k], lo = nzstart[k], hi = nzstart[k + 1];
-        for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort (buckets are small)
-            uint32_t key = t.q2[i];
-            uint32_t j = i;
-            while (j > lo && t.q2[j - 1] > key) { t.q2[j] = t.q2[j - 1]; j--; }
-            t.q2[j] = key;
-        }
         float sum = 0.0f;
-        for (uint32_t i = lo; i < hi; i++) {
-            uint32_t slot = t.q2[i] & 0x7FFFFFFu;
-            sum += __uint_as_float(t.duty[(size_t)slot * 3 + 1]);
+        if (in_lds) {
+            for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort (buckets are small)
+                const uint32_t key = skey[i];
+                const float dc = sdc[i];
+                uint32_t j = i;
+                while (j > lo && skey[j - 1] > key) {
+                    skey[j] = skey[j - 1];
+                    sdc[j] = sdc[j - 1];
+                    j--;
+                }
+                skey[j] = key;
+                sdc[j] = dc;
+            }
+            for (uint32_t i = lo; i < hi; i++) sum += sdc[i];
+        } else {
+            for (uint32_t i = lo + 1; i < hi; i++) {
+                uint32_t key = t.q2[i];
+                uint32_t j = i;
+                while (j > lo && t.q2[j - 1] > key) { t.q2[j] = t.q2[j - 1]; j--; }
+                t.q2[j] = key;
+            }
+            for (uint32_t i = lo; i < hi; i++) {
+                uint32_t slot = t.q2[i] & 0x7FFFFFFu;
+                sum += __uint_as_float(t.duty[(size_t)slot * 3 + 1]);
+            }
         }
         t.colconf[col] = sum;
         if (bm_field(t.infP, col * K, K)) npcol++;
     }
     npcol = wg_sum(sh, npcol);
-    if (threadIdx.x == 0) {
+    // total in nonzero-column order (ascending), sequentially as NuPIC sums
+    // it: wave 0 stages 64 columns per VGPR and folds them lane by lane
+    if (wave_id() == 0) {
         float tot = 0.0f;
-        for (uint32_t k = 0; k < tnz; k++) tot += t.colconf[nzcol[k]];
-        sh->tf[0] = tot;
+        for (uint32_t base = 0; base < tnz; base += 64) {
+            const uint32_t i = base + lane_id();
+            const float v = i < tnz ? t.colconf[nzcol[i]] : 0.0f;
+            const uint32_t m = tnz - base < 64 ? tnz - base : 64;
+            for (uint32_t j = 0; j < m; j++)
+                tot += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+        }
+        if (lane_id() == 0) sh->tf[0] = tot;
     }
     __syncthreads();
     float tot = sh->tf[0];
@@ -1473,13 +1595,17 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
         for (uint32_t j = 0; j < nsyn; j++) atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
     }
     __syncthreads();
-    // exclusive scan over noff entries (chunked per thread)
+    // entries -> 16-byte blocks of 8, then exclusive scan (chunked per thread)
     __shared__ uint32_t part[256];
     __shared__ uint32_t tot;
     const size_t per = (noff + blockDim.x - 1) / blockDim.x;
     const size_t i0 = threadIdx.x * per;
     uint32_t sum = 0;
-    for (size_t k = 0; k < per && i0 + k < noff; k++) sum += off[i0 + k];
+    for (size_t k = 0; k < per && i0 + k < noff; k++) {
+        const uint32_t nb = (off[i0 + k] + 7u) >> 3;
+        off[i0 + k] = nb;
+        sum += nb;
+    }
     part[threadIdx.x] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1502,7 +1628,8 @@ int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// fill: per-(cell, window) cursors in scr_cur
+// fill: per-(cell, window) entry cursors in scr_cur; fx_ent was set to
+// 0xFF.. by the host, so the tail of each list's last block stays padding
 __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
     const int s = blockIdx.x;
     const size_t sc = (size_t)c.seg_cap;
@@ -1511,17 +1638,18 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
     const size_t noff = (size_t)c.ncells * c.fx_nwin + 1;
     const uint32_t* off = b.fx_off + (size_t)s * noff;
     uint32_t* cur = b.scr_cur + (size_t)s * ((size_t)c.ncells * c.fx_nwin);
-    uint32_t* ent = b.fx_ent + b.fx_base[s];
+    uint16_t* ent = reinterpret_cast<uint16_t*>(b.fx_ent + b.fx_base[s]);
     const uint32_t hwm = b.hdr[s].seg_hwm;
-    for (size_t i = threadIdx.x; i + 1 < noff; i += blockDim.x) cur[i] = off[i];
+    const uint32_t W = (uint32_t)c.fx_win;
+    for (size_t i = threadIdx.x; i + 1 < noff; i += blockDim.x) cur[i] = off[i] * 8u;
     __syncthreads();
     for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
         uint32_t m = meta[slot];
         if (!meta_live(m)) continue;
-        uint32_t nsyn = meta_nsyn(m), w = slot / (uint32_t)c.fx_win;
+        uint32_t nsyn = meta_nsyn(m), w = slot / W;
         for (uint32_t j = 0; j < nsyn; j++) {
             uint32_t pos = atomicAdd(&cur[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
-            ent[pos] = slot;
+            ent[pos] = (uint16_t)(slot - w * W);
         }
     }
 }
