@@ -11,6 +11,9 @@ import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd.so")
+# diagnostic build with per-phase cycle stamps (tools/ only): HTM_AMD_STAMPS=1
+if os.environ.get("HTM_AMD_STAMPS") == "1":
+    LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd_stamps.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 HTM_OK = 0
@@ -88,7 +91,7 @@ EXPORTED = [
     "htm_step", "htm_run", "htm_get_output", "htm_output_bytes", "htm_state_bytes", "htm_export_state",
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
-    "htm_profile_read", "htm_counters",
+    "htm_profile_read", "htm_counters", "htm_debug_stamps",
 ]
 
 _lib = None
@@ -153,6 +156,7 @@ def lib():
     L.htm_abi_version.restype = i32
     L.htm_profile_read.argtypes = [vp, P(ctypes.c_double)]
     L.htm_counters.argtypes = [vp, P(ctypes.c_uint64)]
+    L.htm_debug_stamps.argtypes = [vp, P(ctypes.c_uint64)]
     _lib = L
     return L
 

@@ -265,6 +265,9 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->tm.fx_off, uint32_t, S * ((size_t)d.ncells * d.fx_nwin + 1));
     ALLOC(e->d_counts, uint64_t, S);
+#ifdef HTM_STAMPS
+    ALLOC(e->tm.dbg, uint64_t, S * 32);
+#endif
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
     Region* r = e->regions;
@@ -290,11 +293,11 @@ static int allocate(htm_engine* e) {
 
 static int query_lds_optin() {
     int dev = 0, v = 0;
-    hipGetDevice(&dev);
+    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || v <= 0) {
         (void)hipGetLastError();
         v = 65536;
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
     }
     return v;
 }
@@ -333,7 +336,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
         if (mx > 65536) r = fail(HTM_E_HIP, "cannot raise the dynamic LDS limit to %zu B", mx);
     }
     if (r) {
-        for (void* p : e->allocs) hipFree(p);
+        for (void* p : e->allocs) (void)hipFree(p);
         delete e;
         return r;
     }
@@ -364,10 +367,10 @@ int htm_create(const htm_config* cfg, int32_t n_streams, int32_t device, htm_eng
 
 int htm_destroy(htm_engine* e) {
     if (!e) return HTM_OK;
-    hipSetDevice(e->device);
-    hipDeviceSynchronize();
-    for (void* p : e->allocs) hipFree(p);
-    if (e->tm.fx_ent) hipFree(e->tm.fx_ent);
+    (void)hipSetDevice(e->device);
+    (void)hipDeviceSynchronize();
+    for (void* p : e->allocs) (void)hipFree(p);
+    if (e->tm.fx_ent) (void)hipFree(e->tm.fx_ent);
     for (hipEvent_t x : e->ev_pool) (void)hipEventDestroy(x);
     delete e;
     return HTM_OK;
@@ -513,6 +516,19 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
     return HTM_OK;
 }
 
+int htm_debug_stamps(htm_engine* e, uint64_t* out32) {
+    if (!e || !out32) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e->tm.dbg) return fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<uint64_t> h((size_t)e->n * 32);
+    HIP_TRY(hipMemcpy(h.data(), e->tm.dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 32; k++) out32[k] = 0;
+    for (int s = 0; s < e->n; s++)
+        for (int k = 0; k < 32; k++) out32[k] += h[(size_t)s * 32 + k];
+    HIP_TRY(hipMemset(e->tm.dbg, 0, h.size() * 8));
+    return HTM_OK;
+}
+
 int htm_run(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, void* stream) {
     if (!e) return fail(HTM_E_INVALID, "null engine");
     const size_t stride = (size_t)e->n * e->cfg.n_fields;
@@ -643,25 +659,45 @@ int htm_reset_tm(htm_engine* e, void* stream) {
     return HTM_OK;
 }
 
+// Broadcast one stream's slice of a per-stream region into every other
+// stream: a grid-stride copy in 16-byte (or 4-byte / 1-byte) units.
+__global__ void replicate_kernel(uint8_t* base, size_t per, int32_t src, int32_t n, int unit) {
+    const size_t m = per / (size_t)unit;  // units per stream
+    const size_t total = m * (size_t)n;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t s = i / m, k = i - s * m;
+        if ((int32_t)s == src) continue;
+        if (unit == 16)
+            reinterpret_cast<uint4*>(base + per * s)[k] = reinterpret_cast<const uint4*>(base + per * src)[k];
+        else if (unit == 4)
+            reinterpret_cast<uint32_t*>(base + per * s)[k] = reinterpret_cast<const uint32_t*>(base + per * src)[k];
+        else
+            base[per * s + k] = base[per * src + k];
+    }
+}
+
+static int replicate_region(uint8_t* base, size_t per, int32_t src, int32_t n, hipStream_t st) {
+    const int unit = (per % 16 == 0 && ((uintptr_t)base % 16) == 0) ? 16 : (per % 4 == 0 ? 4 : 1);
+    const size_t total = per / unit * (size_t)n;
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(replicate_kernel, dim3((unsigned)blocks), dim3(256), 0, st, base, per, src, n, unit);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     if (!e || src < 0 || src >= e->n) return fail(HTM_E_INVALID, "bad source stream");
     hipStream_t st = (hipStream_t)stream;
     for (int id = 1; id <= 16; id++) {
         const Region& r = e->regions[id];
         if (!r.base) continue;
-        const uint8_t* sp = (const uint8_t*)r.base + r.per_stream * src;
-        for (int s = 0; s < e->n; s++) {
-            if (s == src) continue;
-            HIP_TRY(hipMemcpyAsync((uint8_t*)r.base + r.per_stream * s, sp, r.per_stream, hipMemcpyDeviceToDevice, st));
-        }
+        if (replicate_region((uint8_t*)r.base, r.per_stream, src, e->n, st)) return fail(HTM_E_HIP, "replicate launch");
     }
     // SP active list of the last step too (the TM reads it)
-    for (int s = 0; s < e->n; s++) {
-        if (s == src) continue;
-        HIP_TRY(hipMemcpyAsync(e->sp.act + (size_t)s * HTM_MAXACT, e->sp.act + (size_t)src * HTM_MAXACT,
-                               HTM_MAXACT * 2, hipMemcpyDeviceToDevice, st));
-        HIP_TRY(hipMemcpyAsync(e->sp.nact + s, e->sp.nact + src, 4, hipMemcpyDeviceToDevice, st));
-    }
+    if (replicate_region((uint8_t*)e->sp.act, HTM_MAXACT * 2, src, e->n, st) ||
+        replicate_region((uint8_t*)e->sp.nact, 4, src, e->n, st))
+        return fail(HTM_E_HIP, "replicate launch");
     HIP_TRY(hipStreamSynchronize(st));
     e->fx_valid = false;
     return HTM_OK;

@@ -88,7 +88,30 @@ struct TmBufs {
     uint64_t* fx_base;      // [S] first block of the stream
     uint32_t* fx_off;       // [S][ncells][fx_nwin] + 1 (running block offsets)
     uint4* fx_ent;          // [total blocks] 8 x u16 entries each
+    uint64_t* dbg;          // [S][32] phase stamps + event counts (HTM_STAMPS builds only, else null)
 };
+
+// Diagnostic phase stamps (HTM_STAMPS builds only): thread 0 charges the
+// shader cycles since its previous stamp to bucket k.  Compiled out of the
+// product library.
+#define HTM_NSTAMP 16
+#ifdef HTM_STAMPS
+#define STAMP(t, k)                                                     \
+    do {                                                                \
+        if (threadIdx.x == 0) {                                         \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();         \
+            (t).acc[(k)] += now_ - (t).last;                            \
+            (t).last = now_;                                            \
+        }                                                               \
+    } while (0)
+#define COUNT(t, k, v)                                                  \
+    do {                                                                \
+        if (threadIdx.x == 0) (t).cnt[(k)] += (uint64_t)(v);            \
+    } while (0)
+#else
+#define STAMP(t, k) do { } while (0)
+#define COUNT(t, k, v) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // segment meta word

@@ -83,7 +83,20 @@ struct Tm {
     uint32_t* q2;
     const uint32_t* fxoff;
     const uint4* fxent;
+#ifdef HTM_STAMPS
+    uint64_t acc[HTM_NSTAMP];
+    uint64_t cnt[HTM_NSTAMP];
+    uint64_t last;
+#endif
 };
+
+// stamp buckets (HTM_STAMPS): where one stream-step's cycles go
+enum {
+    SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
+    SB_SCAN
+};
+// event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
+enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS };
 
 // ---------------------------------------------------------------------------
 // LDS layout
@@ -172,7 +185,7 @@ __device__ __forceinline__ uint32_t col_of(const DevCfg& c, uint32_t cell) { ret
 __device__ __forceinline__ uint32_t kmask(int K) { return K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u); }
 
 // Segment::dutyCycle(iteration, active, readOnly=false) on the pool entry
-__device__ float seg_dc_update(uint32_t* duty, uint32_t slot, uint32_t it, bool active) {
+__device__ __forceinline__ float seg_dc_update(uint32_t* duty, uint32_t slot, uint32_t it, bool active) {
     uint32_t* d = duty + (size_t)slot * 3;
     float dc;
     if (it <= kDcTier[1]) {
@@ -197,7 +210,7 @@ __device__ float seg_dc_update(uint32_t* duty, uint32_t slot, uint32_t it, bool 
 
 // ---------------------------------------------------------------------------
 // cell list of a bitmap (ascending) into dst; returns count (uniform)
-__device__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, uint32_t* dst32, uint16_t* dst16, uint32_t cap) {
+__device__ __forceinline__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, uint32_t* dst32, uint16_t* dst16, uint32_t cap) {
     const int cw = t.c.cw;
     const int per = (cw + TM_NT - 1) / TM_NT;
     const int w0 = threadIdx.x * per;
@@ -225,7 +238,7 @@ __device__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, uint32_t* dst32, u
 // ---------------------------------------------------------------------------
 // Inference
 // _inferPhase1(activeColumns, useStartCells)
-__device__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start) {
+__device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start) {
     const int K = t.c.K;
     wg_clear(t.infA, t.c.cw);
     __syncthreads();
@@ -245,12 +258,13 @@ __device__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start
         }
     }
     npc = wg_sum(t.sh, npc);
+    STAMP(t, SB_P1);
     return use_start || (double)npc >= 0.50 * (double)nA;
 }
 
 // collect slots of segments with >= thr synapses onto active cells of
 // `state` by scanning the pool (learning-on form)
-__device__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
+__device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
     const uint32_t hwm = t.sh->hwm;
     const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
     uint32_t nb = 0;  // bytes read by this thread
@@ -281,6 +295,7 @@ __device__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
     }
     nb = wg_sum(t.sh, nb);
     if (threadIdx.x == 0) t.sh->bytes += nb;
+    STAMP(t, SB_SCAN);
 }
 
 // one 16-byte block of a frozen out-list: 8 window-relative u16 slots,
@@ -308,7 +323,7 @@ __device__ __forceinline__ uint32_t fx_find(const uint32_t* pstart, uint32_t lo,
 // concatenated (block prefix in LDS) and each wave streams a contiguous range
 // of that concatenation, 2 x 64 blocks (2 KB) in flight per wave, so the
 // loads are independent of list boundaries and of how skewed out-degrees are.
-__device__ void collect_frozen(Tm& t, int thr) {
+__device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const uint32_t W = (uint32_t)c.fx_win;
@@ -320,6 +335,8 @@ __device__ void collect_frozen(Tm& t, int thr) {
     const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
     const uint32_t na = nact < mac ? nact : mac;
     const uint32_t hwm = sh->hwm;
+    STAMP(t, SB_LIST);
+    COUNT(t, SC_NACT, na);
     const uint32_t nwin = (uint32_t)c.fx_nwin;
     const uint32_t per = (na + TM_NT - 1) / TM_NT;
     const uint32_t k0 = threadIdx.x * per;
@@ -349,6 +366,9 @@ __device__ void collect_frozen(Tm& t, int thr) {
         nblk += B;
         wg_clear(cnt, (int)(W / 4));
         __syncthreads();
+        STAMP(t, SB_WINPRE);
+        COUNT(t, SC_WIN, 1);
+        COUNT(t, SC_BLK, B);
         const uint32_t pw = (B + TM_NWAVES - 1) / TM_NWAVES;
         const uint32_t b0 = wave_id() * pw;
         const uint32_t b1 = b0 + pw < B ? b0 + pw : B;
@@ -373,6 +393,7 @@ __device__ void collect_frozen(Tm& t, int thr) {
             }
         }
         __syncthreads();
+        STAMP(t, SB_STREAM);
         for (uint32_t i = threadIdx.x; i < W / 4; i += TM_NT) {
             uint32_t x = cnt[i];
             if (!x) continue;
@@ -385,6 +406,7 @@ __device__ void collect_frozen(Tm& t, int thr) {
             }
         }
         __syncthreads();
+        STAMP(t, SB_QSCAN);
     }
     // out-list blocks + the two block offsets of every (active cell, window)
     const uint32_t nw = (hwm + W - 1) / W;
@@ -393,7 +415,7 @@ __device__ void collect_frozen(Tm& t, int thr) {
 
 // Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
 // NuPIC order, normalisation.  Returns numPredictedCols (uniform).
-__device__ uint32_t phase2_finish(Tm& t) {
+__device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int K = c.K;
@@ -446,6 +468,9 @@ __device__ uint32_t phase2_finish(Tm& t) {
     }
     nb = wg_sum(sh, nb);
     if (threadIdx.x == 0) sh->bytes += nb;
+    STAMP(t, SB_FIN1);
+    COUNT(t, SC_QN, qn);
+    COUNT(t, SC_P2, 1);
     // exclusive scan of bucket counts + nonzero column list (ascending)
     const int per = (c.ncol + TM_NT - 1) / TM_NT;
     const int c0 = threadIdx.x * per;
@@ -541,12 +566,14 @@ __device__ uint32_t phase2_finish(Tm& t) {
     if (tot > 0.0f)
         for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) t.colconf[nzcol[k]] /= tot;
     __syncthreads();
+    STAMP(t, SB_FIN2);
+    COUNT(t, SC_TNZ, tnz);
     return npcol;
 }
 
 // _inferPhase2()
 template <bool FROZEN>
-__device__ bool infer_phase2(Tm& t) {
+__device__ __forceinline__ bool infer_phase2(Tm& t) {
     TmSh* sh = t.sh;
     if (threadIdx.x == 0) {
         sh->st[0]++;
@@ -573,7 +600,7 @@ __device__ __forceinline__ int lrn_len(Tm& t, int k) { return t.sh->lrn_len[(t.s
 
 // _inferBacktrack(activeColumns)
 template <bool FROZEN>
-__device__ void infer_backtrack(Tm& t) {
+__device__ __forceinline__ void infer_backtrack(Tm& t) {
     TmSh* sh = t.sh;
     const int cw = t.c.cw;
     const int numPrev = sh->n_inf_pat;
@@ -596,6 +623,7 @@ __device__ void infer_backtrack(Tm& t) {
         for (int off = start; off < numPrev; off++) {
             wg_copy(t.infP1, t.infP, cw);
             __syncthreads();
+            STAMP(t, SB_BT);
             inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
             if (!inSeq) break;
             inSeq = infer_phase2<FROZEN>(t);
@@ -639,11 +667,12 @@ __device__ void infer_backtrack(Tm& t) {
     }
     wg_copy(t.infP1, bkP, cw);
     __syncthreads();
+    STAMP(t, SB_BT);
 }
 
 // _updateInferenceState(activeColumns)
 template <bool FROZEN>
-__device__ void update_inference(Tm& t) {
+__device__ __forceinline__ void update_inference(Tm& t) {
     TmSh* sh = t.sh;
     if (threadIdx.x == 0) {
         if (t.c.max_inf_bt > 0) {
@@ -678,7 +707,7 @@ __device__ void update_inference(Tm& t) {
 // per-column best (activity, cellInColumn, first segment) key over the pool
 // for segments with >= thr synapses onto `state`; only columns flagged in
 // `colflags` when it is non-null.  _getBestMatchingCell for many columns.
-__device__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t* colflags) {
+__device__ __forceinline__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t* colflags) {
     const DevCfg& c = t.c;
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
     const uint32_t hwm = t.sh->hwm;
@@ -730,7 +759,7 @@ struct WUpd {
 // _getSegmentActiveSynapses(c, i, s, activeState, newSynapses) with
 // _chooseCellsToLearnFrom; candidates = sh->cand (cells on in `state`).
 // slot == 0xFFFFFFFF: new segment.
-__device__ WUpd w_build_update(Tm& t, uint32_t slot, const uint32_t* state, bool want_new) {
+__device__ __forceinline__ WUpd w_build_update(Tm& t, uint32_t slot, const uint32_t* state, bool want_new) {
     TmSh* sh = t.sh;
     const int l = lane_id();
     const bool exist = slot != 0xFFFFFFFFu;
@@ -796,7 +825,7 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
 }
 
 // _adaptSegment on an existing segment; returns trimSegment (wave-uniform)
-__device__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t n_new, uint32_t my_new) {
+__device__ __forceinline__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t n_new, uint32_t my_new) {
     const DevCfg& c = t.c;
     const int l = lane_id();
     const uint32_t m = t.meta[slot];
@@ -866,7 +895,7 @@ __device__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t 
 }
 
 // _trimSegmentsInCell(c, i, [s], minPermanence=0.00001, minNumSyns=0)
-__device__ void w_trim_segment(Tm& t, uint32_t slot) {
+__device__ __forceinline__ void w_trim_segment(Tm& t, uint32_t slot) {
     const DevCfg& c = t.c;
     const int l = lane_id();
     const uint32_t m = t.meta[slot];
@@ -905,7 +934,7 @@ __device__ void w_trim_segment(Tm& t, uint32_t slot) {
 }
 
 // new sequence segment on `cell` with the chosen sources
-__device__ void w_create_segment(Tm& t, uint32_t cell, uint32_t n_new, uint32_t my_new) {
+__device__ __forceinline__ void w_create_segment(Tm& t, uint32_t cell, uint32_t n_new, uint32_t my_new) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int l = lane_id();
@@ -936,7 +965,7 @@ __device__ void w_create_segment(Tm& t, uint32_t cell, uint32_t n_new, uint32_t 
 }
 
 // _getCellForNewSegment(colIdx); returns the cell index within the column
-__device__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
+__device__ __forceinline__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int l = lane_id();
@@ -992,7 +1021,7 @@ __device__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
 }
 
 // cells on in `bm` -> sh->cand (<= HTM_MAXACT, ascending)
-__device__ void build_cand(Tm& t, const uint32_t* bm) {
+__device__ __forceinline__ void build_cand(Tm& t, const uint32_t* bm) {
     uint32_t n = wg_bitmap_list(t, bm, t.sh->cand, nullptr, HTM_MAXACT);
     if (threadIdx.x == 0) {
         if (n > HTM_MAXACT) { t.sh->err |= 8u; n = HTM_MAXACT; }
@@ -1002,7 +1031,7 @@ __device__ void build_cand(Tm& t, const uint32_t* bm) {
 }
 
 // _processSegmentUpdates(activeColumns)
-__device__ void process_segment_updates(Tm& t, const uint16_t* cols, int nA) {
+__device__ __forceinline__ void process_segment_updates(Tm& t, const uint16_t* cols, int nA) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     wg_clear(t.flags, c.nw);
@@ -1032,7 +1061,7 @@ __device__ void process_segment_updates(Tm& t, const uint16_t* cols, int nA) {
 }
 
 // _learnPhase1(activeColumns, readOnly)
-__device__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA, bool ro) {
+__device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA, bool ro) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int K = c.K;
@@ -1091,7 +1120,7 @@ __device__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA, bool ro) {
 }
 
 // _learnPhase2(readOnly)
-__device__ void learn_phase2(Tm& t, bool ro) {
+__device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int K = c.K;
@@ -1146,7 +1175,7 @@ __device__ void learn_phase2(Tm& t, bool ro) {
 }
 
 // start cells (cell 0) of the given columns into lrnA
-__device__ void set_start_cells(Tm& t, uint32_t* bm, const uint16_t* cols, int nA) {
+__device__ __forceinline__ void set_start_cells(Tm& t, uint32_t* bm, const uint16_t* cols, int nA) {
     wg_clear(bm, t.c.cw);
     __syncthreads();
     for (int a = threadIdx.x; a < nA; a += TM_NT) bm_or_field(bm, (uint32_t)cols[a] * t.c.K, 1, 1u);
@@ -1154,7 +1183,7 @@ __device__ void set_start_cells(Tm& t, uint32_t* bm, const uint16_t* cols, int n
 }
 
 // _learnBacktrackFrom(startOffset, readOnly)
-__device__ bool learn_backtrack_from(Tm& t, int start, bool ro) {
+__device__ __forceinline__ bool learn_backtrack_from(Tm& t, int start, bool ro) {
     TmSh* sh = t.sh;
     const int cw = t.c.cw;
     const int numPrev = sh->n_lrn_pat;
@@ -1184,7 +1213,7 @@ __device__ bool learn_backtrack_from(Tm& t, int start, bool ro) {
 }
 
 // _learnBacktrack(): steps backtracked, 0 on failure
-__device__ int learn_backtrack(Tm& t) {
+__device__ __forceinline__ int learn_backtrack(Tm& t) {
     TmSh* sh = t.sh;
     const int numPrev = sh->n_lrn_pat - 1;
     if (numPrev <= 0) return 0;
@@ -1217,7 +1246,7 @@ __device__ int learn_backtrack(Tm& t) {
 }
 
 // _updateLearningState(activeColumns)
-__device__ void update_learning(Tm& t) {
+__device__ __forceinline__ void update_learning(Tm& t) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     // lrnA1 / lrnP1 hold time t-1 (loaded at entry)
@@ -1276,7 +1305,7 @@ __device__ void update_learning(Tm& t) {
 
 // stable compaction of live segments (slot order preserved) so that a
 // learning step always has seg_reserve free slots
-__device__ void compact_pool(Tm& t) {
+__device__ __forceinline__ void compact_pool(Tm& t) {
     TmSh* sh = t.sh;
     const uint32_t hwm = sh->hwm;
     uint32_t base = 0;
@@ -1374,6 +1403,10 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
         t.fxoff = nullptr;
         t.fxent = nullptr;
     }
+#ifdef HTM_STAMPS
+    for (int k = 0; k < HTM_NSTAMP; k++) t.acc[k] = t.cnt[k] = 0;
+    t.last = __builtin_amdgcn_s_memtime();
+#endif
     TmSh* sh = t.sh;
     htm_tm_header* hdr = b.hdr + s;
     uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
@@ -1466,10 +1499,13 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
         }
     }
     __syncthreads();
+    STAMP(t, SB_LOAD);
     if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) compact_pool(t);
     // ---- BacktrackingTM.compute(input, learn, infer=True)
     update_inference<FROZEN>(t);
+    STAMP(t, SB_BT);
     if (LEARN) update_learning(t);
+    STAMP(t, SB_LEARN);
     // ---- write back
     __syncthreads();
     wg_copy(gbm, t.infA, c.cw);
@@ -1520,6 +1556,18 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
         hdr->stat_lrn_phase2 = sh->st[2];
         hdr->stat_lrn_backtrack = sh->st[3];
     }
+#ifdef HTM_STAMPS
+    __syncthreads();
+    STAMP(t, SB_WB);
+    COUNT(t, SC_STEPS, 1);
+    if (threadIdx.x == 0 && b.dbg) {
+        uint64_t* d = b.dbg + (size_t)s * 32;
+        for (int k = 0; k < HTM_NSTAMP; k++) {
+            d[k] += t.acc[k];
+            d[16 + k] += t.cnt[k];
+        }
+    }
+#endif
 }
 
 int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen, int n,

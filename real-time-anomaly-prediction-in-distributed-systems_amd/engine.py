@@ -179,6 +179,16 @@ class HTMEngine:
                 "seg_hwm", "error"]
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def debug_stamps(self) -> dict:
+        """Per-phase TM cycle stamps + event counts (diagnostic stamps build only)."""
+        out = (ctypes.c_uint64 * 32)()
+        check(self._L.htm_debug_stamps(self.h, out))
+        names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
+                 "scan"]
+        cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
+        return dict(cycles={k: int(out[i]) for i, k in enumerate(names)},
+                    counts={k: int(out[16 + i]) for i, k in enumerate(cnames)})
+
     def frozen_index_valid(self) -> bool:
         return bool(self._L.htm_frozen_index_valid(self.h))
 

@@ -1,0 +1,480 @@
+"""Drop-in batched counterpart of the NuPIC network surface the reference uses.
+
+The reference builds one `nupic.engine.Network` per model and drives it one
+record at a time (ML/HTM/NetworkModel.py:48-157, NetworkUtils.py:111-163):
+
+    network = Network()
+    network.addRegion("sensorRegion", "py.RecordSensor", json.dumps({...}))
+    network.regions["sensorRegion"].getSelf().encoder = createEncoder()
+    network.addRegion("l1SpatialPoolerRegion", "py.SPRegion", json.dumps(SP_PARAMS))
+    network.link("sensorRegion", "l1SpatialPoolerRegion", "UniformLink", "")
+    ...
+    dataSource.setData(cpu)                          # StreamReader.py:157-161
+    network.run(1)                                   # NetworkModel.py:127
+    score = network.regions[TM].getOutputData("anomalyScore")[0]   # :133
+    network.save("network1.nta"); Network("network1.nta")          # NetworkUtils.py:156-163
+
+This module keeps exactly that call pattern, but one `Network` steps
+`n_streams` independent copies of the graph in lockstep on one MI355X through
+the HIP engine (`HTMEngine`, include/htm_amd.h).  Every output is batched
+along a leading stream axis; element 0 is stream 0, so single-stream code
+that indexes `[0]` keeps working unchanged.
+
+Scope: RecordSensor (ScalarEncoder / MultiEncoder),
+SPRegion and TMRegion are executed by the engine; an SDRClassifierRegion may
+be added (NetworkModel.py:86-97 does) but is inert: its outputs raise, as the
+classifier is not on the anomaly hot path.
+Errors follow the NuPIC convention of raising (NTA_THROW -> RuntimeError /
+ValueError); there is no CPU fallback -- creating the engine fails loudly if
+the HIP library or a GPU is missing.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import numpy as np
+
+from . import _lib
+
+SENSOR, SP, TM, CLASSIFIER = "py.RecordSensor", "py.SPRegion", "py.TMRegion", "py.SDRClassifierRegion"
+_ENGINE_FILE = "engine.htm"
+_META_FILE = "network.json"
+
+
+# ---------------------------------------------------------------- encoders
+class ScalarEncoder:
+    """nupic.encoders.ScalarEncoder parameters (non-periodic, as the reference
+    configures it: NetworkUtils.py:80-88).  Encoding itself runs on the GPU
+    (sp.hip enc_first_on_bit); the host side only answers bucket queries for
+    the sensor's bucketIdxOut output."""
+
+    def __init__(self, w, minval, maxval, n=0, clipInput=False, name=None, fieldname=None, periodic=False,
+                 radius=0, resolution=0, forced=False, verbosity=0):
+        if periodic:
+            raise ValueError("periodic ScalarEncoder is not supported")
+        if radius or resolution:
+            raise ValueError("ScalarEncoder: only the n/w form used by the reference is supported")
+        if n <= w:
+            raise ValueError("ScalarEncoder: n must be > w")
+        if maxval <= minval:
+            raise ValueError("ScalarEncoder: maxval must be > minval")
+        self.w, self.n = int(w), int(n)
+        self.minval, self.maxval = float(minval), float(maxval)
+        self.clipInput = bool(clipInput)
+        self.name = name if name is not None else "[%s:%s]" % (minval, maxval)
+        self.fieldname = fieldname if fieldname is not None else self.name
+        self.resolution = (self.maxval - self.minval) / float(self.n - self.w)
+        self.halfwidth = (self.w - 1) // 2
+
+    def getWidth(self):
+        return self.n
+
+    def getBucketIndices(self, x):
+        """[minbin] or [None] for a missing value (ScalarEncoder._getFirstOnBit)."""
+        if x is None or (isinstance(x, float) and math.isnan(x)):
+            return [None]
+        x = float(x)
+        if x < self.minval:
+            if not self.clipInput:
+                raise ValueError("input %s less than minval %s" % (x, self.minval))
+            x = self.minval
+        if x > self.maxval:
+            if not self.clipInput:
+                raise ValueError("input %s greater than maxval %s" % (x, self.maxval))
+            x = self.maxval
+        centerbin = int((x - self.minval + self.resolution / 2.0) / self.resolution) + self.halfwidth
+        return [centerbin - self.halfwidth]
+
+    def bucket_indices(self, xs: np.ndarray) -> np.ndarray:
+        """Vectorised getBucketIndices over a batch (missing -> -1)."""
+        x = np.asarray(xs, dtype=np.float64)
+        miss = np.isnan(x)
+        if not self.clipInput and np.any(~miss & ((x < self.minval) | (x > self.maxval))):
+            raise ValueError("input outside [minval, maxval] with clipInput False")
+        xc = np.clip(np.where(miss, self.minval, x), self.minval, self.maxval)
+        b = ((xc - self.minval + self.resolution / 2.0) / self.resolution).astype(np.int64)
+        return np.where(miss, -1, b)
+
+
+class MultiEncoder:
+    """nupic.encoders.MultiEncoder: sub-encoders concatenated in sorted field
+    name order (NetworkUtils.py:77-108)."""
+
+    def __init__(self, encoderDefinitions=None):
+        self.encoders = {}
+        if encoderDefinitions:
+            self.addMultipleEncoders(encoderDefinitions)
+
+    def addEncoder(self, name, encoder):
+        self.encoders[name] = encoder
+
+    def addMultipleEncoders(self, fieldEncodings):
+        for key in sorted(fieldEncodings):
+            spec = dict(fieldEncodings[key])
+            kind = spec.pop("type", "ScalarEncoder")
+            if kind != "ScalarEncoder":
+                raise ValueError("encoder type %s is not supported (ScalarEncoder only)" % kind)
+            fieldname = spec.pop("fieldname", key)
+            name = spec.pop("name", key)
+            self.addEncoder(key, ScalarEncoder(name=name, fieldname=fieldname, **spec))
+
+    def fields(self):
+        return [self.encoders[k] for k in sorted(self.encoders)]
+
+    def getWidth(self):
+        return sum(e.getWidth() for e in self.fields())
+
+
+# ----------------------------------------------------------- data source
+class BatchRecordStream:
+    """Batched stand-in for the reference's kafkaRecordStream
+    (ML/HTM/StreamReader.py:64-230).  The reference hands one value per field
+    to the sensor through module globals (setData :157-161, grabStreamData
+    :179-188); here each network owns its stream object and `setData` takes
+    one value (or an array of n_streams values) per field.  None / NaN are
+    missing values (SENTINEL_VALUE_FOR_MISSING_DATA -> all-zero SDR)."""
+
+    def __init__(self, names=("cpu",), n_streams=1):
+        self.names = list(names)
+        self.n_streams = int(n_streams)
+        self._values = None
+        self._recordCount = 0
+
+    def setData(self, dataRec, memRec=None):
+        fields = [dataRec] if memRec is None else [dataRec, memRec]
+        cols = []
+        for f in fields:
+            if isinstance(f, np.ndarray) and f.dtype.kind in "fiu":
+                a = f.astype(np.float64).ravel()
+            else:
+                a = np.asarray([np.nan if f is None else f] if np.ndim(f) == 0 else f, dtype=object)
+                a = np.array([np.nan if v is None else float(v) for v in a.ravel()], dtype=np.float64)
+            if a.size == 1 and self.n_streams > 1:
+                a = np.full(self.n_streams, a[0])
+            if a.size != self.n_streams:
+                raise ValueError("setData: expected %d values per field, got %d" % (self.n_streams, a.size))
+            cols.append(a)
+        self._values = np.stack(cols, axis=1)  # [n_streams, fields]
+
+    def getNextRecord(self):
+        if self._values is None:
+            raise RuntimeError("no data: call setData() before network.run()")
+        self._recordCount += 1
+        return self._values
+
+    def rewind(self):
+        self._recordCount = 0
+
+    def getNextRecordIdx(self):
+        return self._recordCount
+
+
+# ------------------------------------------------------------------ regions
+class _RegionImpl:
+    """getSelf() object of a region (holds parameters and host attributes)."""
+
+    def __init__(self, params):
+        self.params = dict(params)
+
+
+class _SensorImpl(_RegionImpl):
+    def __init__(self, params):
+        super().__init__(params)
+        self.encoder = None
+        self.dataSource = None
+        self.predictedField = None
+        self.values = None  # [n_streams, fields] of the last run
+
+
+class _ClassifierImpl(_RegionImpl):
+    def __init__(self, params):
+        super().__init__(params)
+        steps = str(params.get("steps", "1"))
+        self.stepsList = [int(x) for x in steps.split(",") if x.strip()]
+        self.maxCategoryCount = 0
+
+
+class Region:
+    """network.regions[name]: setParameter / getParameter / getOutputData /
+    getSelf, as the reference calls them (NetworkUtils.py:116-152,
+    NetworkModel.py:41-44,129-133)."""
+
+    _MODES = {
+        SENSOR: {"predictedField", "verbosity"},
+        SP: {"learningMode", "inferenceMode", "anomalyMode", "topDownMode"},
+        TM: {"learningMode", "inferenceMode", "anomalyMode", "topDownMode"},
+        CLASSIFIER: {"learningMode", "inferenceMode"},
+    }
+
+    def __init__(self, network, name, node_type, params):
+        self.network = network
+        self.name = name
+        self.type = node_type
+        self.modes = {"learningMode": True, "inferenceMode": True, "anomalyMode": False, "topDownMode": False}
+        self._impl = {SENSOR: _SensorImpl, CLASSIFIER: _ClassifierImpl}.get(node_type, _RegionImpl)(params)
+
+    def getSelf(self):
+        return self._impl
+
+    def setParameter(self, name, value):
+        if name not in self._MODES[self.type]:
+            raise ValueError("region %s (%s) has no settable parameter %r" % (self.name, self.type, name))
+        if self.type == SENSOR:
+            setattr(self._impl, name, value)
+            return
+        if self.type == TM and name == "inferenceMode" and not value:
+            raise ValueError("TMRegion inferenceMode False is not supported (the anomaly score needs inference)")
+        self.modes[name] = bool(value)
+        if name == "learningMode":
+            self.network._learning_changed()
+
+    def getParameter(self, name):
+        if self.type == SENSOR:
+            return getattr(self._impl, name)
+        if name in self.modes:
+            return self.modes[name]
+        return self._impl.params[name]
+
+    def getOutputData(self, name):
+        return self.network._output(self, name)
+
+
+# ------------------------------------------------------------------ network
+# reference parameter names -> htm_config fields (NetworkUtils.py:26-64)
+_SP_MAP = {"columnCount": "sp_columns", "numActiveColumnsPerInhArea": "sp_num_active",
+           "potentialPct": "sp_potential_pct", "synPermConnected": "sp_perm_connected",
+           "synPermActiveInc": "sp_perm_active_inc", "synPermInactiveDec": "sp_perm_inactive_dec",
+           "minPctOverlapDutyCycle": "sp_min_pct_overlap_dc", "dutyCyclePeriod": "sp_duty_cycle_period",
+           "boostStrength": "sp_boost_strength", "stimulusThreshold": "sp_stimulus_threshold", "seed": "sp_seed"}
+_TM_MAP = {"cellsPerColumn": "tm_cells_per_col", "newSynapseCount": "tm_new_syn_count",
+           "maxSynapsesPerSegment": "tm_max_syn_per_seg", "maxSegmentsPerCell": "tm_max_segs_per_cell",
+           "initialPerm": "tm_initial_perm", "connectedPerm": "tm_connected_perm",
+           "permanenceInc": "tm_perm_inc", "permanenceDec": "tm_perm_dec", "permanenceMax": "tm_perm_max",
+           "minThreshold": "tm_min_threshold", "activationThreshold": "tm_activation_threshold",
+           "pamLength": "tm_pam_length", "maxInfBacktrack": "tm_max_inf_backtrack",
+           "maxLrnBacktrack": "tm_max_lrn_backtrack", "maxSeqLength": "tm_max_seq_length",
+           "segUpdateValidDuration": "tm_seg_update_valid_duration", "seed": "tm_seed"}
+# parameters accepted only at the value the engine implements
+_SP_FIXED = {"globalInhibition": 1, "spatialImp": "cpp", "localAreaDensity": -1.0, "wrapAround": True}
+_TM_FIXED = {"globalDecay": 0.0, "maxAge": 0, "outputType": "normal", "temporalImp": "cpp", "doPooling": False,
+             "burnIn": 2, "collectStats": False}
+_IGNORED = {"spVerbosity", "verbosity", "inputWidth", "columnCount", "potentialRadius", "spatialImp",
+            "temporalImp"}
+
+
+def engine_config(sensor_enc: MultiEncoder, sp_params: dict, tm_params: dict, **engine_opts):
+    """Translate the reference's region parameter dicts into an htm_config
+    (raises ValueError for anything the engine does not implement)."""
+    fields = sensor_enc.fields()
+    if not fields:
+        raise ValueError("the sensor has no encoder (NetworkUtils.createEncoder)")
+    e0 = fields[0]
+    for e in fields[1:]:
+        if (e.n, e.w, e.minval, e.maxval, e.clipInput) != (e0.n, e0.w, e0.minval, e0.maxval, e0.clipInput):
+            raise ValueError("all encoder fields must share n/w/minval/maxval/clipInput")
+    over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_minval=e0.minval, enc_maxval=e0.maxval,
+                enc_clip=int(e0.clipInput))
+    for params, mapping, fixed, region in ((sp_params, _SP_MAP, _SP_FIXED, "SPRegion"),
+                                           (tm_params, _TM_MAP, _TM_FIXED, "TMRegion")):
+        for k, v in params.items():
+            if k in mapping:
+                over[mapping[k]] = v
+            elif k in fixed:
+                if v != fixed[k] and not (isinstance(v, (int, float)) and float(v) == float(fixed[k])):
+                    raise ValueError("%s %s=%r is not supported (only %r)" % (region, k, v, fixed[k]))
+            elif k not in _IGNORED:
+                raise ValueError("%s parameter %r is not supported" % (region, k))
+    width = sensor_enc.getWidth()
+    if int(sp_params.get("inputWidth", 0) or width) != width:
+        raise ValueError("SPRegion inputWidth %s != encoder width %d" % (sp_params.get("inputWidth"), width))
+    cols = int(sp_params.get("columnCount", 2048))
+    if int(tm_params.get("columnCount", cols)) != cols or int(tm_params.get("inputWidth", cols)) != cols:
+        raise ValueError("TMRegion columnCount/inputWidth must equal the SP columnCount")
+    over.update(engine_opts)
+    return _lib.default_config(**over)
+
+
+class Network:
+    """Batched nupic.engine.Network: `Network()` builds an empty graph,
+    `Network(path)` loads a saved one (ModelTesting.py:176)."""
+
+    def __init__(self, path: str | None = None, n_streams: int = 1, device: int | None = None, **engine_opts):
+        self.regions = {}
+        self.links = []
+        self.n_streams = int(n_streams)
+        self.device = device
+        self.engine_opts = dict(engine_opts)
+        self.engine = None
+        self._scores = None
+        self._learn_dirty = False
+        if path is not None:
+            self._load(path)
+
+    # ------------------------------------------------------------ building
+    def addRegion(self, name, nodeType, nodeParams="{}"):
+        if self.engine is not None:
+            raise RuntimeError("cannot add regions after the network is initialized")
+        if name in self.regions:
+            raise ValueError("region %r already exists" % name)
+        if nodeType not in (SENSOR, SP, TM, CLASSIFIER):
+            raise ValueError("region type %r is not supported by the MI355X engine" % nodeType)
+        params = json.loads(nodeParams) if isinstance(nodeParams, str) else dict(nodeParams or {})
+        r = Region(self, name, nodeType, params)
+        self.regions[name] = r
+        return r
+
+    def link(self, srcName, destName, linkType="UniformLink", linkParams="", srcOutput=None, destInput=None):
+        for n in (srcName, destName):
+            if n not in self.regions:
+                raise ValueError("unknown region %r" % n)
+        if linkType != "UniformLink":
+            raise ValueError("link type %r is not supported" % linkType)
+        self.links.append((srcName, destName, srcOutput or "bottomUpOut", destInput or "bottomUpIn"))
+
+    def _find(self, kind):
+        rs = [r for r in self.regions.values() if r.type == kind]
+        if len(rs) != 1:
+            raise RuntimeError("the engine runs exactly one %s per network (found %d)" % (kind, len(rs)))
+        return rs[0]
+
+    def _check_graph(self):
+        sensor, sp, tm = self._find(SENSOR), self._find(SP), self._find(TM)
+        feed = {(s, d) for s, d, so, di in self.links if so == "bottomUpOut" or (so == "dataOut")}
+        feed |= {(s, d) for s, d, so, di in self.links if di == "bottomUpIn"}
+        if (sensor.name, sp.name) not in feed or (sp.name, tm.name) not in feed:
+            raise RuntimeError("the graph must link sensor -> SPRegion -> TMRegion (NetworkModel.py:61,67)")
+        return sensor, sp, tm
+
+    def initialize(self):
+        if self.engine is not None:
+            return
+        from .engine import HTMEngine
+        sensor, sp, tm = self._check_graph()
+        enc = sensor.getSelf().encoder
+        if enc is None:
+            raise RuntimeError("sensor %r has no encoder" % sensor.name)
+        if isinstance(enc, ScalarEncoder):
+            m = MultiEncoder()
+            m.addEncoder(enc.name, enc)
+            enc = m
+        cfg = engine_config(enc, sp.getSelf().params, tm.getSelf().params, **self.engine_opts)
+        self.engine = HTMEngine(self.n_streams, config=cfg, device=self.device)
+        self._learning_changed()
+
+    def _learning_changed(self):
+        self._learn_dirty = True
+
+    def _apply_learning(self):
+        if self._learn_dirty and self.engine is not None:
+            sp, tm = self._find(SP), self._find(TM)
+            self.engine.set_learning(sp.modes["learningMode"], tm.modes["learningMode"])
+            self._learn_dirty = False
+
+    # ------------------------------------------------------------- running
+    def run(self, n):
+        """network.run(n): n lockstep steps of every stream (NetworkModel.py:127).
+        Each step pulls one record (a value per stream and field) from the
+        sensor's data source, like RecordSensor.compute does."""
+        self.initialize()
+        self._apply_learning()
+        import torch
+        sensor = self._find(SENSOR).getSelf()
+        if sensor.dataSource is None:
+            raise RuntimeError("sensor has no dataSource")
+        for _ in range(int(n)):
+            vals = np.asarray(sensor.dataSource.getNextRecord(), dtype=np.float64)
+            if vals.shape != (self.n_streams, self.engine.n_fields):
+                raise ValueError("record shape %s != (%d streams, %d fields)" %
+                                 (vals.shape, self.n_streams, self.engine.n_fields))
+            sensor.values = vals
+            self._scores = self.engine.step(torch.from_numpy(np.ascontiguousarray(vals).ravel()))
+
+    def _output(self, region, name):
+        if self.engine is None:
+            raise RuntimeError("network has not run yet")
+        eng = self.engine
+        if region.type == SENSOR:
+            vals = region.getSelf().values
+            if vals is None:
+                raise RuntimeError("network has not run yet")
+            if name == "actValueOut":
+                return vals[:, 0].astype(np.float64)
+            if name == "bucketIdxOut":
+                enc = region.getSelf().encoder
+                e = enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
+                return e.bucket_indices(vals[:, 0]).astype(np.float64)
+            if name == "sourceOut":
+                return vals.copy()
+        elif region.type == SP:
+            if name == "bottomUpOut":
+                return eng.get_output("active_columns").cpu().numpy().astype(np.float32)
+        elif region.type == TM:
+            if name == "anomalyScore":
+                if not region.modes["anomalyMode"]:
+                    raise RuntimeError("anomalyScore needs anomalyMode True (NetworkUtils.py:152)")
+                return self._scores.cpu().numpy()
+            if name == "bottomUpOut":
+                return eng.bitmap_to_dense(eng.get_output("tm_output")).astype(np.float32)
+            if name == "topDownOut":
+                return eng.get_output("col_confidence").cpu().numpy()
+            if name in ("activeCells", "lrnActiveStateT"):
+                return eng.bitmap_to_dense(eng.get_output("inf_active" if name == "activeCells" else "lrn_active"))
+            if name == "predictedActiveCells":
+                a = eng.bitmap_to_dense(eng.get_output("inf_active"))
+                return a & eng.bitmap_to_dense(eng.get_output("inf_predicted"))
+        elif region.type == CLASSIFIER:
+            raise NotImplementedError("SDRClassifierRegion outputs are not computed by the MI355X engine "
+                                      "(not on the anomaly path; SURVEY.md §8(f)-3)")
+        raise ValueError("region %s (%s) has no output %r" % (region.name, region.type, name))
+
+    def scores_tensor(self):
+        """Device tensor of the last step's anomaly scores (no host copy)."""
+        return self._scores
+
+    # ----------------------------------------------------------- save/load
+    def save(self, path):
+        """network.save(path) (NetworkUtils.py:156-159): a bundle directory like
+        NuPIC's .nta -- network.json (regions, parameters, links, modes) plus
+        engine.htm (every stream's SP/TM state, htm_save)."""
+        self.initialize()
+        self._apply_learning()
+        os.makedirs(path, exist_ok=True)
+        meta = {"n_streams": self.n_streams, "links": self.links, "regions": []}
+        for r in self.regions.values():
+            ent = {"name": r.name, "type": r.type, "params": r.getSelf().params, "modes": r.modes}
+            if r.type == SENSOR:
+                enc = r.getSelf().encoder
+                fields = enc.fields() if isinstance(enc, MultiEncoder) else [enc]
+                ent["encoder"] = [dict(key=f.name, fieldname=f.fieldname, n=f.n, w=f.w, minval=f.minval,
+                                       maxval=f.maxval, clipInput=f.clipInput) for f in fields]
+                ent["predictedField"] = r.getSelf().predictedField
+            meta["regions"].append(ent)
+        with open(os.path.join(path, _META_FILE), "w") as f:
+            json.dump(meta, f, indent=1)
+        self.engine.save(os.path.join(path, _ENGINE_FILE))
+        return path
+
+    def _load(self, path):
+        from .engine import HTMEngine
+        with open(os.path.join(path, _META_FILE)) as f:
+            meta = json.load(f)
+        self.n_streams = int(meta["n_streams"])
+        for ent in meta["regions"]:
+            r = self.addRegion(ent["name"], ent["type"], ent["params"])
+            r.modes.update(ent["modes"])
+            if ent["type"] == SENSOR:
+                enc = MultiEncoder()
+                for e in ent["encoder"]:
+                    enc.addEncoder(e["key"], ScalarEncoder(w=e["w"], minval=e["minval"], maxval=e["maxval"],
+                                                           n=e["n"], clipInput=e["clipInput"], name=e["key"],
+                                                           fieldname=e["fieldname"]))
+                r.getSelf().encoder = enc
+                r.getSelf().predictedField = ent.get("predictedField")
+        self.links = [tuple(x) for x in meta["links"]]
+        self.engine = HTMEngine.load(os.path.join(path, _ENGINE_FILE), device=self.device)
+        if self.engine.n_streams != self.n_streams:
+            raise RuntimeError("engine file holds %d streams, network.json says %d" %
+                               (self.engine.n_streams, self.n_streams))
+        self._learn_dirty = True

@@ -1,0 +1,142 @@
+"""The batched Network facade (network.py): host-side logic on CPU, and the
+reference's Model-1 call pattern driven through it on the GPU."""
+import os
+
+import numpy as np
+import pytest
+
+import reference_model1 as ref
+from conftest import GOLDEN
+
+
+def test_reference_params_translate_to_the_default_config(rt):
+    enc = ref.create_encoder(rt)
+    cfg = rt.network.engine_config(enc, dict(ref.SP_PARAMS, inputWidth=500), ref.TM_PARAMS)
+    assert cfg.as_dict() == rt.default_config().as_dict()
+
+
+def test_two_field_encoder_config(rt):
+    enc = ref.create_encoder(rt, multilevel=True)
+    assert enc.getWidth() == 1000 and [f.name for f in enc.fields()] == ["cpu", "mem"]
+    cfg = rt.network.engine_config(enc, dict(ref.SP_PARAMS, inputWidth=1000), ref.TM_PARAMS)
+    assert cfg.n_fields == 2
+
+
+@pytest.mark.parametrize("region,key,val", [("sp", "globalInhibition", 0), ("tm", "globalDecay", 0.1),
+                                            ("tm", "maxAge", 100000), ("tm", "outputType", "activeState1CellPerCol"),
+                                            ("sp", "potentialRadius_x", 3), ("tm", "doPooling", True)])
+def test_unsupported_parameters_raise(rt, region, key, val):
+    enc = ref.create_encoder(rt)
+    sp, tm = dict(ref.SP_PARAMS, inputWidth=500), dict(ref.TM_PARAMS)
+    (sp if region == "sp" else tm)[key] = val
+    with pytest.raises(ValueError):
+        rt.network.engine_config(enc, sp, tm)
+
+
+def test_input_width_mismatch_raises(rt):
+    with pytest.raises(ValueError):
+        rt.network.engine_config(ref.create_encoder(rt), dict(ref.SP_PARAMS, inputWidth=400), ref.TM_PARAMS)
+
+
+def test_scalar_encoder_buckets_match_the_oracle(rt, oracle_mod):
+    enc = ref.create_encoder(rt).fields()[0]
+    m = oracle_mod.OracleModel()
+    xs = np.concatenate([np.arange(-5, 106, 0.25), [np.nan, 33.3333, 0.104, 99.9]])
+    b = enc.bucket_indices(xs)
+    for x, bi in zip(xs, b):
+        sdr = m.encode([x])
+        on = np.nonzero(sdr)[0]
+        if np.isnan(x):
+            assert bi == -1 and len(on) == 0
+        else:
+            assert on[0] == bi and len(on) == 21 and enc.getBucketIndices(float(x)) == [bi]
+
+
+def test_record_stream_batches_and_missing_values(rt):
+    ds = rt.BatchRecordStream(["cpu"], n_streams=3)
+    ds.setData([1.0, None, 3])
+    v = ds.getNextRecord()
+    assert v.shape == (3, 1) and np.isnan(v[1, 0]) and v[2, 0] == 3.0
+    ds.setData(np.array([4, 5, 6]), np.array([7.0, 8.0, 9.0]))
+    assert ds.getNextRecord().shape == (3, 2)
+    ds.setData(42)  # scalar broadcast to every stream
+    assert np.all(ds.getNextRecord() == 42)
+    with pytest.raises(ValueError):
+        ds.setData([1, 2])
+
+
+def test_graph_errors_are_raised_before_any_gpu_work(rt):
+    net = rt.Network()
+    net.addRegion("s", "py.RecordSensor", "{}")
+    with pytest.raises(ValueError):
+        net.addRegion("s", "py.SPRegion", "{}")
+    with pytest.raises(ValueError):
+        net.addRegion("x", "py.KNNClassifierRegion", "{}")
+    with pytest.raises(ValueError):
+        net.link("s", "nope", "UniformLink", "")
+    with pytest.raises(ValueError):
+        net.regions["s"].setParameter("learningMode", True)
+    with pytest.raises(RuntimeError):
+        net.run(1)  # no SP/TM regions
+
+
+@pytest.mark.gpu
+def test_model1_through_the_facade_matches_golden(rt, traces, tmp_path):
+    """ModelTraining/ModelTesting's call pattern through the drop-in surface:
+    setData -> run(1) -> getOutputData('anomalyScore')[0], save before the
+    2185th step, reload with Network(path), TM learning off."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    g = np.load(os.path.join(GOLDEN, "model1_golden.npz"))
+    ds = rt.BatchRecordStream(["cpu"])
+    net = ref.create_one_level_network(rt, ds, seg_capacity=72 * 1024)
+    tmr = net.regions[ref.TMR]
+    got = []
+    for k, cpu in enumerate(traces["train"][:2184]):
+        ds.setData(float(cpu))
+        net.run(1)
+        got.append(tmr.getOutputData("anomalyScore")[0])
+        if k == 0:
+            act = net.regions[ref.SPR].getOutputData("bottomUpOut")[0]
+            assert np.array_equal(np.nonzero(act)[0], np.sort(g["train_active"][0]))
+            assert net.regions[ref.SENSOR].getOutputData("actValueOut")[0] == cpu
+    assert np.array_equal(np.array(got, np.float32), g["train_scores"])
+    path = net.save(str(tmp_path / "network1.nta"))
+    net2 = rt.Network(path)
+    ds2 = rt.BatchRecordStream(["cpu"])
+    net2.regions[ref.SENSOR].getSelf().dataSource = ds2
+    tm2 = net2.regions[ref.TMR]
+    for r, cpu in enumerate(traces["test"][:40]):
+        win = []
+        for j in range(8):
+            ds2.setData(float(cpu))
+            if j == 0:
+                tm2.setParameter("learningMode", False)  # NetworkModel.py:40-44
+            net2.run(1)
+            win.append(tm2.getOutputData("anomalyScore")[0])
+        assert np.array_equal(np.array(win, np.float32), g["test_windows"][r])
+    with pytest.raises(NotImplementedError):
+        net2.regions[ref.CLS].getOutputData("probabilities")
+
+
+@pytest.mark.gpu
+def test_batched_facade_streams_are_independent(rt, traces):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    n = 4
+    ds = rt.BatchRecordStream(["cpu"], n_streams=n)
+    net = ref.create_one_level_network(rt, ds, n_streams=n, seg_capacity=1 << 13)
+    ds1 = rt.BatchRecordStream(["cpu"])
+    one = ref.create_one_level_network(rt, ds1, seg_capacity=1 << 13)
+    rng = np.random.default_rng(11)
+    for k in range(60):
+        v = np.clip(traces["train"][k] + rng.integers(-3, 4, size=n), 0, 100).astype(np.float64)
+        ds.setData(v)
+        net.run(1)
+        ds1.setData(float(v[2]))
+        one.run(1)
+        a = net.regions[ref.TMR].getOutputData("anomalyScore")
+        assert a.shape == (n,)
+        assert a[2] == one.regions[ref.TMR].getOutputData("anomalyScore")[0]
