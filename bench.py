@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--seg-capacity", type=int, default=72 * 1024)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--mode", choices=["step", "run"], default="step",
+                    help="step: one htm_step (network.run(1) of every stream) per step, lockstep; "
+                         "run: the K steps as htm_run replay chunks (each stream runs ahead independently)")
     args = ap.parse_args()
 
     import torch
@@ -112,14 +115,16 @@ def main():
 
     S = args.streams
     n_total = S * world
+    s0, s1 = rt.fleet.shard_range(n_total, world, rank)
     eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals)
     eng.set_learning(False, False)
     T = args.warmup + args.steps
-    vals = torch.tensor(make_inputs(n_total, rank * S, (rank + 1) * S, 0, T, trace), device=f"cuda:{local}")
+    vals = torch.tensor(make_inputs(n_total, s0, s1, 0, T, trace), device=f"cuda:{local}")
     scores = torch.empty((T, S), dtype=torch.float32, device=f"cuda:{local}")
+    gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
     gathered = None
-    if world > 1:
-        gathered = torch.empty((args.steps, world, S), dtype=torch.float32, device=f"cuda:{local}") if rank == 0 else None
+    if world > 1 and rank == 0:
+        gathered = torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}")
 
     for k in range(args.warmup):
         eng.step(vals[k], out=scores[k])
@@ -132,11 +137,18 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     handles = []
-    for k in range(args.steps):
-        eng.step(vals[args.warmup + k], out=scores[args.warmup + k])
+    if args.mode == "run":
+        eng.run(vals[args.warmup:], out=scores[args.warmup:])
         if world > 1:
-            gl = list(gathered[k].unbind(0)) if rank == 0 else None
-            handles.append(dist.gather(scores[args.warmup + k], gather_list=gl, dst=0, async_op=True))
+            for k in range(args.steps):
+                h, _ = gather.gather(scores[args.warmup + k], staging=gathered[k] if rank == 0 else None)
+                handles.append(h)
+    else:
+        for k in range(args.steps):
+            eng.step(vals[args.warmup + k], out=scores[args.warmup + k])
+            if world > 1:
+                h, _ = gather.gather(scores[args.warmup + k], staging=gathered[k] if rank == 0 else None)
+                handles.append(h)
     for h in handles:
         h.wait()
     torch.cuda.synchronize()
@@ -157,13 +169,15 @@ def main():
     roof = None
     if prof is not None and prof["tm_ms"] > 0:
         tm_bytes = c1["tm_bytes"] - c0["tm_bytes"]
-        launches = prof["steps"]
+        launches = prof["launches"]
         avg_ms = prof["tm_ms"] / launches
         achieved = tm_bytes / launches / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "tm_step_kernel<learn=false,frozen=true>",
-                "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": int(tm_bytes / launches),
+                "kernel": ("htm_run_kernel<false,true> (fused SP+TM)" if prof["sp_ms"] == 0
+                           else "tm_step_kernel<false,true>"),
+                "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
+                "bytes_per_launch": int(tm_bytes / launches),
                 "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "stream-steps/s", "n_gpus": world,
@@ -172,6 +186,7 @@ def main():
         "data": "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config 2)",
         "config": {"workload": "config2: Model-1 streams (2048-col SP, 12-cell BacktrackingTM), SP+TM learn off, "
                                "from the GPU-trained Model-1 state",
+                   "mode": args.mode,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": 2048, "cells_per_column": 12,
                    "trained_segments": int(hdr.seg_live), "train_s": round(train_s, 2),
                    "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL gather of scores" if world > 1 else "")},

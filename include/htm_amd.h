@@ -117,10 +117,15 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
 #define HTM_OPT_KEEP_PREV 2    /* 1: retain prevPredictedColumns for HTM_OUT_PREV_PRED_COLS */
 #define HTM_OPT_KEEP_OVERLAPS 3 /* 1: retain SP overlaps for HTM_OUT_SP_OVERLAPS */
 #define HTM_OPT_PROFILE 4       /* 1: bracket each step's SP and TM kernels with HIP events */
+#define HTM_OPT_FUSED 5         /* 1 (default): one fused SP+TM kernel per htm_step and per
+                                   chunk of htm_run steps (each stream runs its chunk without
+                                   waiting for the others); 0: separate SP and TM launches */
+#define HTM_OPT_RUN_CHUNK 6     /* steps per fused htm_run launch (default 256) */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
-/* Kernel times of the profiled steps since the last call (synchronises):
- * out4 = {SP kernel ms, TM kernel ms, profiled steps, 0}. */
+/* Kernel times of the profiled launches since the last call (synchronises):
+ * out4 = {SP kernel ms, TM (or fused SP+TM) kernel ms, steps covered,
+ * profiled launches}.  Fused launches report their whole time as TM. */
 int htm_profile_read(htm_engine* eng, double* out4);
 
 /* Sum over streams of the TM counters (synchronises): out8 = {algorithmic HBM

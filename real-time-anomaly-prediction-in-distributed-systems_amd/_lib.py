@@ -32,6 +32,8 @@ OPT_FROZEN_INDEX = 1
 OPT_KEEP_PREV = 2
 OPT_KEEP_OVERLAPS = 3
 OPT_PROFILE = 4
+OPT_FUSED = 5
+OPT_RUN_CHUNK = 6
 
 
 class HtmConfig(ctypes.Structure):

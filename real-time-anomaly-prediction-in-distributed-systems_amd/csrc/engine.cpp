@@ -66,7 +66,10 @@ struct htm_engine {
     Region regions[17];
     int32_t profile = 0;
     std::vector<hipEvent_t> ev_pool;
+    std::vector<int32_t> ev_steps;  // steps covered by each profiled event triple
     size_t ev_used = 0;
+    int32_t fused = 1;              // HTM_OPT_FUSED
+    int32_t run_chunk = 256;        // steps per fused htm_run launch
 };
 
 extern "C" {
@@ -135,6 +138,9 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
         c.tm_max_lrn_backtrack > HTM_MAXPAT - 1)
         return fail(HTM_E_INVALID, "backtrack depth must be 0..15");
     if (c.tm_pam_length < 1) return fail(HTM_E_INVALID, "pamLength must be > 0");
+    if (c.tm_activation_threshold < 1 || c.tm_activation_threshold > HTM_MAXSYN || c.tm_min_threshold < 1 ||
+        c.tm_min_threshold > HTM_MAXSYN)
+        return fail(HTM_E_INVALID, "activation/min thresholds must be 1..32");
     if (c.seg_capacity < 64 || c.seg_capacity > (1 << 27)) return fail(HTM_E_INVALID, "seg_capacity");
     if (c.upd_capacity < 1 || c.upd_capacity > 65535) return fail(HTM_E_INVALID, "upd_capacity");
     std::memset(&d, 0, sizeof(d));
@@ -195,6 +201,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.n_streams = n;
     d.max_act_cells = d.num_desired * d.K;
     d.q_lds = 1024;
+    d.fin_sorted = 1;
+    if (const char* env = std::getenv("HTM_TM_FIN")) d.fin_sorted = std::strcmp(env, "buckets") != 0;
     // frozen-inference counter window: the union region holds the u8
     // counters (fx_win bytes) plus the active-cell list and its block prefix;
     // fill the LDS budget (two workgroups per CU by default).  Out-list
@@ -210,6 +218,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     if (win > capr) win = capr;
     d.fx_win = (int32_t)win;
     d.fx_nwin = (int32_t)((d.seg_cap + d.fx_win - 1) / d.fx_win);
+    d.fx_pcap = d.fx_win < 65535 ? d.fx_win : 65535;
+    d.fx_noff = d.ncells * d.fx_nwin + d.ncells + 1;
     return HTM_OK;
 }
 
@@ -260,10 +270,13 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.scr_conf, float, S * d.ncol);
     ALLOC(e->tm.scr_q, uint32_t, S * cap);
     ALLOC(e->tm.scr_q2, uint32_t, S * cap);
-    ALLOC(e->tm.scr_cur, uint32_t, S * (size_t)d.ncells * d.fx_nwin);
+    ALLOC(e->tm.scr_cur, uint32_t, S * (size_t)d.fx_noff);
     ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
     ALLOC(e->tm.fx_base, uint64_t, S);
-    ALLOC(e->tm.fx_off, uint32_t, S * ((size_t)d.ncells * d.fx_nwin + 1));
+    ALLOC(e->tm.fx_off, uint32_t, S * (size_t)d.fx_noff);
+    ALLOC(e->tm.fx_rec, uint2, S * cap);
+    ALLOC(e->tm.fx_pcell, uint16_t, S * (size_t)d.fx_pcap);
+    ALLOC(e->tm.fx_np, uint32_t, S);
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
     ALLOC(e->tm.dbg, uint64_t, S * 32);
@@ -327,6 +340,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
         long v = std::strtol(env, nullptr, 10);
         if (v >= 16384 && v <= optin) budget = (size_t)v;
     }
+    if (const char* env = std::getenv("HTM_FUSED")) e->fused = std::atoi(env) != 0;  // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (!r) r = check_lds(e->dc);
     if (!r) r = allocate(e);
@@ -392,6 +406,12 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
     else if (opt == HTM_OPT_PROFILE) {
         e->profile = value ? 1 : 0;
         e->ev_used = 0;
+        e->ev_steps.clear();
+    }
+    else if (opt == HTM_OPT_FUSED) e->fused = value ? 1 : 0;
+    else if (opt == HTM_OPT_RUN_CHUNK) {
+        if (value < 1) return fail(HTM_E_INVALID, "run chunk must be >= 1");
+        e->run_chunk = value;
     }
     else return fail(HTM_E_INVALID, "unknown option %d", opt);
     return HTM_OK;
@@ -429,7 +449,7 @@ static int build_fx(htm_engine* e, hipStream_t st) {
 
 extern "C" {
 
-static int next_events(htm_engine* e, hipEvent_t* ev) {
+static int next_events(htm_engine* e, hipEvent_t* ev, int32_t steps) {
     // three events per profiled step: before SP, between SP and TM, after TM
     while (e->ev_pool.size() < e->ev_used + 3) {
         hipEvent_t x;
@@ -438,13 +458,14 @@ static int next_events(htm_engine* e, hipEvent_t* ev) {
     }
     for (int k = 0; k < 3; k++) ev[k] = e->ev_pool[e->ev_used + k];
     e->ev_used += 3;
+    e->ev_steps.push_back(steps);
     return HTM_OK;
 }
 
-int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
-    if (!e || !d_values || !d_scores) return fail(HTM_E_INVALID, "bad arguments");
-    hipStream_t st = (hipStream_t)stream;
-    int frozen = 0;
+// Mode of the next steps: the TM kernel variant follows the learning flags;
+// with TM learning off the frozen forward index is (re)built first.
+static int prepare_step(htm_engine* e, hipStream_t st, int* frozen) {
+    *frozen = 0;
     if (e->tm_learn) {
         e->fx_valid = false;
     } else if (e->use_frozen) {
@@ -452,11 +473,38 @@ int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* strea
             int r = build_fx(e, st);
             if (r) return r;
         }
-        frozen = 1;
+        *frozen = 1;
     }
+    return HTM_OK;
+}
+
+// n_steps network.run(1) of every stream in one fused SP+TM launch.
+static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, hipStream_t st,
+                     int frozen) {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     if (e->profile) {
-        int r = next_events(e, ev);
+        int r = next_events(e, ev, n_steps);
+        if (r) return r;
+        HIP_TRY(hipEventRecord(ev[0], st));
+        HIP_TRY(hipEventRecord(ev[1], st));
+    }
+    if (launch_htm_run(e->dc, e->tm, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
+                       e->keep_prev, e->keep_overlaps, e->n, st))
+        return fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
+    if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
+    return HTM_OK;
+}
+
+int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
+    if (!e || !d_values || !d_scores) return fail(HTM_E_INVALID, "bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    int frozen = 0;
+    int r = prepare_step(e, st, &frozen);
+    if (r) return r;
+    if (e->fused) return run_fused(e, 1, d_values, d_scores, st, frozen);
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (e->profile) {
+        r = next_events(e, ev, 1);
         if (r) return r;
         HIP_TRY(hipEventRecord(ev[0], st));
     }
@@ -486,11 +534,14 @@ int htm_profile_read(htm_engine* e, double* out4) {
         sp += a;
         tm += b;
     }
+    double steps = 0.0;
+    for (int32_t x : e->ev_steps) steps += x;
     out4[0] = sp;
     out4[1] = tm;
-    out4[2] = (double)(e->ev_used / 3);
-    out4[3] = 0.0;
+    out4[2] = steps;
+    out4[3] = (double)(e->ev_used / 3);
     e->ev_used = 0;
+    e->ev_steps.clear();
     return HTM_OK;
 }
 
@@ -531,7 +582,20 @@ int htm_debug_stamps(htm_engine* e, uint64_t* out32) {
 
 int htm_run(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, void* stream) {
     if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (n_steps < 0 || (n_steps > 0 && (!d_values || !d_scores))) return fail(HTM_E_INVALID, "bad arguments");
     const size_t stride = (size_t)e->n * e->cfg.n_fields;
+    if (e->fused) {
+        hipStream_t st = (hipStream_t)stream;
+        int frozen = 0;
+        int r = prepare_step(e, st, &frozen);
+        if (r) return r;
+        for (int32_t k = 0; k < n_steps; k += e->run_chunk) {
+            const int32_t m = n_steps - k < e->run_chunk ? n_steps - k : e->run_chunk;
+            r = run_fused(e, m, d_values + (size_t)k * stride, d_scores + (size_t)k * e->n, st, frozen);
+            if (r) return r;
+        }
+        return HTM_OK;
+    }
     for (int32_t k = 0; k < n_steps; k++) {
         int r = htm_step(e, d_values + (size_t)k * stride, d_scores + (size_t)k * e->n, stream);
         if (r) return r;

@@ -43,7 +43,10 @@ struct DevCfg {
     int32_t seg_reserve;                  // free slots needed before a learning step
     int32_t fx_win;                       // frozen index: segments per LDS counter window (<= 65536)
     int32_t fx_nwin;                      // windows covering seg_cap
+    int32_t fx_pcap;                      // frozen index: max predictive-capable segments (pid space)
+    int32_t fx_noff;                      // fx_off entries per stream: ncells*fx_nwin + ncells + 1
     int32_t q_lds;                        // qualifying segments sorted in LDS (more: global path)
+    int32_t fin_sorted;                   // phase-2 tail: 1 bitonic key sort, 0 column buckets (tuning knob)
     int32_t max_act_cells;                // num_desired * K (frozen collection cell list)
     int32_t n_streams;
 };
@@ -85,9 +88,19 @@ struct TmBufs {
     // segments with a synapse from x fill the 16-byte blocks
     // fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1]), padded
     // with 0xFFFF, so one uint4 load delivers 8 entries of one list
+    // The same block pool also holds, per cell, the list of predictive-
+    // capable segment ids (pid: live segments with >= activationThreshold
+    // connected synapses, numbered densely in slot order) that the cell
+    // feeds through a CONNECTED synapse, so frozen phase 2 counts connected
+    // activity without reading synapse rows.  fx_rec holds what phase 2
+    // needs of a qualifying segment: its cell and the dutyCycle value it
+    // reads while learning is off (the iteration counter is frozen).
     uint64_t* fx_base;      // [S] first block of the stream
-    uint32_t* fx_off;       // [S][ncells][fx_nwin] + 1 (running block offsets)
+    uint32_t* fx_off;       // [S][fx_noff]: [cell][window] lists, then [cell] pid lists, then the end
     uint4* fx_ent;          // [total blocks] 8 x u16 entries each
+    uint2* fx_rec;          // [S][seg_cap] {cell, dutyCycle bits}
+    uint16_t* fx_pcell;     // [S][fx_pcap] cell of each pid
+    uint32_t* fx_np;        // [S] number of pids (> fx_pcap: pid lists not built, rows are read)
     uint64_t* dbg;          // [S][32] phase stamps + event counts (HTM_STAMPS builds only, else null)
 };
 
@@ -100,13 +113,13 @@ struct TmBufs {
     do {                                                                \
         if (threadIdx.x == 0) {                                         \
             const uint64_t now_ = __builtin_amdgcn_s_memtime();         \
-            (t).acc[(k)] += now_ - (t).last;                            \
-            (t).last = now_;                                            \
+            (t).sh->st_acc[(k)] += now_ - (t).sh->st_last;              \
+            (t).sh->st_last = now_;                                     \
         }                                                               \
     } while (0)
 #define COUNT(t, k, v)                                                  \
     do {                                                                \
-        if (threadIdx.x == 0) (t).cnt[(k)] += (uint64_t)(v);            \
+        if (threadIdx.x == 0) (t).sh->st_cnt[(k)] += (uint64_t)(v);     \
     } while (0)
 #else
 #define STAMP(t, k) do { } while (0)
@@ -246,6 +259,9 @@ int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int l
 int launch_tm_init(const DevCfg& c, const TmBufs& b, const uint64_t* seeds, int n, hipStream_t st);
 int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen,
                    int n, hipStream_t st);
+int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
+                   int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
+                   hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

@@ -16,23 +16,7 @@
 //     highest-index tie break -- the nupic.core ">=" insertion order;
 //   * learning touches only the active columns' potential permanences
 //     (float32, potential order) and flips connected bits with atomicXor.
-#include "htm_dev.h"
-
-// ScalarEncoder._getFirstOnBit (double arithmetic, NaN -> missing)
-__device__ __forceinline__ int enc_first_on_bit(const DevCfg& c, double x) {
-    if (isnan(x)) return -1;
-    if (x < c.enc_min) {
-        if (!c.enc_clip) return -1;
-        x = c.enc_min;
-    }
-    if (x > c.enc_max) {
-        if (!c.enc_clip) return -1;
-        x = c.enc_max;
-    }
-    double q = __ddiv_rn(__dadd_rn(__dadd_rn(x, -c.enc_min), __ddiv_rn(c.enc_resolution, 2.0)), c.enc_resolution);
-    int centerbin = (int)q + c.enc_halfwidth;
-    return centerbin - c.enc_halfwidth;
-}
+#include "sp_dev.h"
 
 // ---------------------------------------------------------------------------
 // SP initialisation: one lane per stream runs nupic::Random sequentially.
@@ -102,245 +86,10 @@ int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
-// Overlap + global inhibition by wave 0.  Lane l owns words l and l+64.
-struct SpShared {
-    uint32_t in[64];           // input SDR bits (nin_pad <= 2048)
-    uint32_t act[HTM_MAXNW];   // active columns bitmap
-    uint32_t ovnz[HTM_MAXNW];  // overlap > 0
-    int32_t act_inputs[256];   // active input rows
-    uint16_t actlist[HTM_MAXACT];
-    int32_t n_act_inputs;
-    int32_t nact;
-    uint32_t iter;
-    int32_t nbump;
-    uint16_t bump[HTM_MAXNW * 32 > 4096 ? 4096 : HTM_MAXNW * 32];
-    float red[4];
-};
-
-__device__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SpShared& sh, int write_overlaps) {
-    const int l = lane_id();
-    const int nw = c.nw;
-    uint32_t p0[HTM_NPLANES], p1[HTM_NPLANES];
-#pragma unroll
-    for (int k = 0; k < HTM_NPLANES; k++) { p0[k] = 0; p1[k] = 0; }
-    const uint32_t* connT = b.connT + (size_t)s * c.nin_pad * nw;
-    const int nai = sh.n_act_inputs;
-    for (int a = 0; a < nai; a++) {
-        const uint32_t* row = connT + (size_t)sh.act_inputs[a] * nw;
-        uint32_t x0 = l < nw ? row[l] : 0u;
-        uint32_t x1 = (l + 64) < nw ? row[l + 64] : 0u;
-#pragma unroll
-        for (int k = 0; k < HTM_NPLANES; k++) {
-            uint32_t t0 = p0[k] & x0, t1 = p1[k] & x1;
-            p0[k] ^= x0; p1[k] ^= x1;
-            x0 = t0; x1 = t1;
-        }
-    }
-    // eligibility: overlap >= stimulusThreshold (bit-sliced compare)
-    uint32_t gt0 = 0, gt1 = 0, eq0 = ~0u, eq1 = ~0u;
-    for (int k = HTM_NPLANES - 1; k >= 0; k--) {
-        if ((c.stim_thr >> k) & 1) { eq0 &= p0[k]; eq1 &= p1[k]; }
-        else { gt0 |= eq0 & p0[k]; gt1 |= eq1 & p1[k]; eq0 &= ~p0[k]; eq1 &= ~p1[k]; }
-    }
-    uint32_t cand0 = (gt0 | eq0) & (l < nw ? ~0u : 0u);
-    uint32_t cand1 = (gt1 | eq1) & ((l + 64) < nw ? ~0u : 0u);
-    uint32_t win0 = 0, win1 = 0;
-    uint32_t need = (uint32_t)c.num_desired;
-    for (int k = HTM_NPLANES - 1; k >= 0; k--) {
-        uint32_t h0 = cand0 & p0[k], h1 = cand1 & p1[k];
-        uint32_t cnt = wave_sum_u32((uint32_t)(__popc(h0) + __popc(h1)));
-        if (cnt >= need) {
-            cand0 = h0; cand1 = h1;
-        } else {
-            win0 |= h0; win1 |= h1;
-            need -= cnt;
-            cand0 &= ~p0[k]; cand1 &= ~p1[k];
-        }
-    }
-    // ties at the threshold: the `need` highest column indices win.  Words
-    // are ordered w = l (< 64) then l + 64; suffix counts over word index.
-    uint32_t pc0 = __popc(cand0), pc1 = __popc(cand1);
-    // suffix sum over words > w: total over all - inclusive prefix
-    uint32_t incl1 = wave_incl_scan(pc1);
-    uint32_t tot1 = __shfl(incl1, 63, 64);
-    uint32_t incl0 = wave_incl_scan(pc0);
-    uint32_t tot0 = __shfl(incl0, 63, 64);
-    uint32_t above1 = tot1 - incl1;            // words l+65.. in the upper half
-    uint32_t above0 = tot1 + (tot0 - incl0);   // whole upper half + words l+1..63
-    // take = clamp(need - above, 0, popcount) in signed arithmetic
-    int r1 = (int)need - (int)above1, r0 = (int)need - (int)above0;
-    r1 = r1 < 0 ? 0 : (r1 > (int)pc1 ? (int)pc1 : r1);
-    r0 = r0 < 0 ? 0 : (r0 > (int)pc0 ? (int)pc0 : r0);
-    const uint32_t take1 = (uint32_t)r1, take0 = (uint32_t)r0;
-    uint32_t keep0 = 0, keep1 = 0;
-    for (uint32_t j = 0; j < take0; j++) { uint32_t pos = 31 - __clz(cand0); keep0 |= 1u << pos; cand0 &= ~(1u << pos); }
-    for (uint32_t j = 0; j < take1; j++) { uint32_t pos = 31 - __clz(cand1); keep1 |= 1u << pos; cand1 &= ~(1u << pos); }
-    uint32_t a0 = win0 | keep0, a1 = win1 | keep1;
-    uint32_t nz0 = 0, nz1 = 0;
-#pragma unroll
-    for (int k = 0; k < HTM_NPLANES; k++) { nz0 |= p0[k]; nz1 |= p1[k]; }
-    if (l < nw) { sh.act[l] = a0; sh.ovnz[l] = nz0; }
-    if (l + 64 < nw) { sh.act[l + 64] = a1; sh.ovnz[l + 64] = nz1; }
-    // ascending active list
-    uint32_t q0 = __popc(a0), q1 = __popc(a1);
-    uint32_t e0 = wave_incl_scan(q0) - q0;
-    uint32_t t0 = __shfl(e0 + q0, 63, 64);
-    uint32_t e1 = t0 + wave_incl_scan(q1) - q1;
-    uint32_t pos = e0;
-    for (uint32_t x = a0; x; x &= x - 1) { if (pos < HTM_MAXACT) sh.actlist[pos] = (uint16_t)(l * 32 + __ffs(x) - 1); pos++; }
-    pos = e1;
-    for (uint32_t x = a1; x; x &= x - 1) { if (pos < HTM_MAXACT) sh.actlist[pos] = (uint16_t)((l + 64) * 32 + __ffs(x) - 1); pos++; }
-    uint32_t total = __shfl(e1 + q1, 63, 64);
-    if (l == 0) sh.nact = (int32_t)total;
-    if (write_overlaps) {
-        int32_t* ov = b.overlaps + (size_t)s * c.ncol;
-        for (int bit = 0; bit < 32; bit++) {
-            if (l < nw) {
-                int32_t v = 0;
-#pragma unroll
-                for (int k = 0; k < HTM_NPLANES; k++) v |= (int32_t)((p0[k] >> bit) & 1u) << k;
-                ov[l * 32 + bit] = v;
-            }
-            if (l + 64 < nw) {
-                int32_t v = 0;
-#pragma unroll
-                for (int k = 0; k < HTM_NPLANES; k++) v |= (int32_t)((p1[k] >> bit) & 1u) << k;
-                ov[(l + 64) * 32 + bit] = v;
-            }
-        }
-    }
-}
-
-// updatePermanencesForColumn_ on one potential permanence: returns the new
-// value and whether it is connected (>= synPermConnected - epsilon, tested
-// after the raise-clip and before the trim-clip).
-__device__ __forceinline__ float sp_update_perm(const DevCfg& c, float p, bool raise, bool& isconn) {
-    if (raise) {
-        p = p > 1.0f ? 1.0f : p;
-        p = p < 0.0f ? 0.0f : p;
-    }
-    isconn = p >= c.sp_conn_thr;
-    p = p > 1.0f ? 1.0f : p;
-    p = p < c.sp_trim ? 0.0f : p;
-    return p;
-}
-
-// One wave adapts one column: lane l owns inputs [8l, 8l+8) of each 512-bit
-// chunk of the potential mask.  mode 0: adaptSynapses_ (+inc/-dec by input),
-// mode 1: bumpUpWeakColumns_ (+synPermBelowStimulusInc, no raise).
-__device__ void sp_adapt_column(const DevCfg& c, const SpBufs& b, int s, int col, const uint32_t* in_bits, int mode) {
-    const int l = lane_id();
-    const int pw = c.nin_pad >> 5;
-    const uint32_t* prow = b.potmask + ((size_t)s * c.ncol + col) * pw;
-    float* perm = b.perm + ((size_t)s * c.ncol + col) * c.n_potential;
-    uint32_t* connT = b.connT + (size_t)s * c.nin_pad * c.nw;
-    const uint32_t cw = (uint32_t)col >> 5, cb = 1u << (col & 31);
-    int rank_base = 0;
-    for (int chunk = 0; chunk < pw; chunk += 16) {  // 16 words = 512 inputs per pass
-        int wi = chunk + (l >> 2);
-        uint32_t byte = 0, ibyte = 0;
-        if (wi < pw) {
-            byte = (prow[wi] >> ((l & 3) * 8)) & 0xFFu;
-            ibyte = (in_bits[wi] >> ((l & 3) * 8)) & 0xFFu;
-        }
-        uint32_t pc = __popc(byte);
-        uint32_t incl = wave_incl_scan(pc);
-        uint32_t r = rank_base + incl - pc;
-        for (uint32_t x = byte; x; x &= x - 1) {
-            int j = __ffs(x) - 1;
-            int input = (chunk + (l >> 2)) * 32 + (l & 3) * 8 + j;
-            float p = perm[r];
-            bool oldc = p >= c.sp_conn_thr;
-            if (mode == 0) p = p + (((ibyte >> j) & 1u) ? c.sp_inc : -1 * c.sp_dec);
-            else p = p + c.sp_below_inc;
-            bool newc;
-            p = sp_update_perm(c, p, mode == 0, newc);
-            perm[r] = p;
-            if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
-            r++;
-        }
-        rank_base += __shfl(incl, 63, 64);
-    }
-}
-
 template <bool LEARN>
 __global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps) {
-    const int s = blockIdx.x;
     __shared__ SpShared sh;
-    const int t = threadIdx.x;
-    const int pw = c.nin_pad >> 5;
-    // ---- encoder (RecordSensor -> MultiEncoder.encodeIntoArray)
-    if (t < 64) sh.in[t] = 0;
-    if (t == 0) {
-        int n = 0;
-        for (int f = 0; f < c.n_fields; f++) {
-            int bkt = enc_first_on_bit(c, values[(size_t)s * c.n_fields + f]);
-            if (bkt < 0) continue;
-            for (int k = 0; k < c.enc_w; k++) sh.act_inputs[n++] = f * c.enc_n + bkt + k;
-        }
-        sh.n_act_inputs = n;
-        uint32_t* sc = b.scalars + (size_t)s * 4;
-        uint32_t it = sc[0] + 1;  // updateBookeepingVars_
-        sc[0] = it;
-        if (LEARN) sc[1] = sc[1] + 1;
-        sh.iter = it;
-    }
-    __syncthreads();
-    for (int k = t; k < sh.n_act_inputs; k += blockDim.x) {
-        int i = sh.act_inputs[k];
-        atomicOr(&sh.in[i >> 5], 1u << (i & 31));
-    }
-    __syncthreads();
-    if (t < 64) sp_overlap_inhibit(c, b, s, sh, write_overlaps);
-    __syncthreads();
-    const int nact = sh.nact < HTM_MAXACT ? sh.nact : HTM_MAXACT;
-    if (t < nact) b.act[(size_t)s * HTM_MAXACT + t] = sh.actlist[t];
-    if (t == 0) b.nact[s] = (uint32_t)nact;
-    if (!LEARN) return;
-    // ---- adaptSynapses_: one wave per active column
-    for (int a = wave_id(); a < nact; a += blockDim.x >> 6) sp_adapt_column(c, b, s, sh.actlist[a], sh.in, 0);
-    __syncthreads();
-    // ---- updateDutyCycles_ (period = min(dutyCyclePeriod, iterationNum))
-    float* odc = b.duty + (size_t)s * 2 * c.ncol;
-    float* adc = odc + c.ncol;
-    const uint32_t period = (uint32_t)c.dc_period > sh.iter ? sh.iter : (uint32_t)c.dc_period;
-    const float pm1 = (float)(period - 1), pf = (float)period;
-    float min_odc = __uint_as_float(b.scalars[(size_t)s * 4 + 2]);
-    if (t == 0) sh.nbump = 0;
-    __syncthreads();
-    float mx = 0.0f;
-    for (int col = t; col < c.ncol; col += blockDim.x) {
-        float ov = (float)((sh.ovnz[col >> 5] >> (col & 31)) & 1u);
-        float ac = (float)((sh.act[col >> 5] >> (col & 31)) & 1u);
-        float o = (odc[col] * pm1 + ov) / pf;
-        float a = (adc[col] * pm1 + ac) / pf;
-        odc[col] = o;
-        adc[col] = a;
-        mx = o > mx ? o : mx;
-        if (o < min_odc) {  // bumpUpWeakColumns_ candidates
-            int k = atomicAdd(&sh.nbump, 1);
-            sh.bump[k] = (uint16_t)col;
-        }
-    }
-    // boost factors: exp((target - activeDutyCycle) * 0) == 1 (boostStrength 0)
-    __syncthreads();
-    const int nb = sh.nbump;
-    if (nb > 0) {
-        // ascending order is irrelevant: each column is updated independently
-        for (int k = wave_id(); k < nb; k += blockDim.x >> 6) sp_adapt_column(c, b, s, sh.bump[k], sh.in, 1);
-    }
-    // ---- isUpdateRound_: updateMinDutyCyclesGlobal_
-    if (sh.iter % (uint32_t)c.update_period == 0) {
-        mx = __uint_as_float(wave_max_u32(__float_as_uint(mx)));  // non-negative floats order as uints
-        if (lane_id() == 0) sh.red[wave_id()] = mx;
-        __syncthreads();
-        if (t == 0) {
-            float m = sh.red[0];
-            for (int w = 1; w < (int)(blockDim.x >> 6); w++) m = sh.red[w] > m ? sh.red[w] : m;
-            b.scalars[(size_t)s * 4 + 2] = __float_as_uint(c.sp_min_pct_odc * m);
-        }
-    }
-    (void)pw;
+    sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps);
 }
 
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,

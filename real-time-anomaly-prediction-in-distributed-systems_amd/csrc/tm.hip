@@ -26,10 +26,13 @@
 //     bit-identical to the oracle;
 //   * the data-dependent nupic::Random draws of learning run on lane 0 of
 //     wave 0 in NuPIC order; everything else is wave- or workgroup-parallel.
-#include "htm_dev.h"
+#include "sp_dev.h"
 
 #define TM_NT 256
 #define TM_NWAVES (TM_NT / 64)
+#define FX_DEPTH 8                 // out-list blocks in flight per thread
+#define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
+#define FX_MAXPER 8                // active cells per thread (<= 64 columns x 32 cells / TM_NT)
 
 __constant__ float kDcAlpha[9] = {0.0f, 0.0032f, 0.0010f, 0.00032f, 0.00010f, 0.000032f, 0.00001f, 0.0000032f, 0.0000010f};
 __constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 100000, 320000};
@@ -58,6 +61,9 @@ struct __attribute__((aligned(16))) TmSh {
     uint32_t newsrc[HTM_MAXSYN];
     uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
     uint16_t lrn_pat[HTM_MAXPAT][HTM_MAXACT];
+#ifdef HTM_STAMPS
+    uint64_t st_acc[HTM_NSTAMP], st_cnt[HTM_NSTAMP], st_last, st_start;
+#endif
 };
 
 struct Tm {
@@ -83,20 +89,20 @@ struct Tm {
     uint32_t* q2;
     const uint32_t* fxoff;
     const uint4* fxent;
-#ifdef HTM_STAMPS
-    uint64_t acc[HTM_NSTAMP];
-    uint64_t cnt[HTM_NSTAMP];
-    uint64_t last;
-#endif
+    const uint2* fxrec;
+    const uint16_t* fxpcell;
+    uint32_t np;       // predictive-capable segments (pids) of this stream
 };
 
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN
+    SB_SCAN, SB_SORT, SB_SUMS
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
-enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS };
+// and a histogram of whole-step cycles: SC_HIST + b counts steps of
+// [2^(15+b), 2^(16+b)) cycles (b = 0 also holds shorter ones, b = 8 longer)
+enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
 
 // ---------------------------------------------------------------------------
 // LDS layout
@@ -124,14 +130,19 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     //          qualifying-segment buffers qkey/qdc/skey/sdc[q_lds]
     //  keys (learning): best-match keys u64[ncol]
     //  frozen collection: u8 counters[fx_win], active cells u16[max_act_cells],
-    //          block prefix u32[max_act_cells+1]
+    //          block prefix u32[max_act_cells+1], list starts u32[max_act_cells],
+    //          block -> list map u16[FX_OWN]
     //  trim flags (learning): u32[upd_cap]
     size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
                  (size_t)(c.q_lds + 1) / 2;
     size_t keys = learn ? 2 * (size_t)c.ncol : 0;
-    size_t col = frozen ? (size_t)c.fx_win / 4 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells + 1 : 0;
+    size_t col = frozen ? (size_t)c.fx_win / 4 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells + 1 +
+                              FX_OWN / 2
+                        : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
+    size_t spw = (sizeof(SpShared) + 3) / 4;  // the fused kernels' SP step
     size_t u = fin;
+    if (spw > u) u = spw;
     if (keys > u) u = keys;
     if (col > u) u = col;
     if (trim > u) u = trim;
@@ -147,7 +158,12 @@ size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen) { return tm_layo
 // ---------------------------------------------------------------------------
 // workgroup helpers
 __device__ __forceinline__ void wg_clear(uint32_t* p, int n) {
-    for (int i = threadIdx.x; i < n; i += TM_NT) p[i] = 0;
+    if ((((uintptr_t)p) & 15) == 0 && (n & 3) == 0) {
+        uint4* p4 = reinterpret_cast<uint4*>(p);
+        for (int i = threadIdx.x; i < (n >> 2); i += TM_NT) p4[i] = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+        for (int i = threadIdx.x; i < n; i += TM_NT) p[i] = 0;
+    }
 }
 __device__ __forceinline__ void wg_copy(uint32_t* d, const uint32_t* s, int n) {
     for (int i = threadIdx.x; i < n; i += TM_NT) d[i] = s[i];
@@ -309,20 +325,136 @@ __device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v) {
     }
 }
 
-// containing list of block b: k in [lo, hi) with pstart[k] <= b < pstart[k+1]
-__device__ __forceinline__ uint32_t fx_find(const uint32_t* pstart, uint32_t lo, uint32_t hi, uint32_t b) {
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pstart[mid] <= b) lo = mid; else hi = mid;
+// the same, and every counter that reaches thr (it happens once: counters
+// only grow) appends base + slot to dst at *qn -- qualification without a
+// sweep over the counters
+__device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint32_t thr, uint32_t base, int32_t* qn,
+                                                    uint32_t* dst) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t old[8];
+#pragma unroll
+    for (int h = 0; h < 8; h++) {
+        const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+        old[h] = rel != 0xFFFFu ? atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8)) : 0u;
     }
-    return lo;
+#pragma unroll
+    for (int h = 0; h < 8; h++) {
+        const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+        if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) dst[atomicAdd(qn, 1)] = base + rel;
+    }
 }
 
-// learning-off form: forward propagation over the frozen cell->segment index.
-// Per window of the slot space, the out-lists of the active cells are
-// concatenated (block prefix in LDS) and each wave streams a contiguous range
-// of that concatenation, 2 x 64 blocks (2 KB) in flight per wave, so the
-// loads are independent of list boundaries and of how skewed out-degrees are.
+// Stream the 16-byte blocks of lists k < na -- list k is the block range
+// [plo[k], plo[k] + n_k) of ent, pstart the exclusive prefix of n_k with
+// pstart[na] = B -- and count every u16 entry into the u8 counters.  Per
+// pass a block -> list map is built in LDS, then every thread issues its
+// FX_DEPTH block loads before counting any, so one HBM round trip covers
+// FX_OWN blocks whatever the list lengths.
+template <bool PUSH>
+__device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
+                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t thr = 0,
+                                          uint32_t base = 0, int32_t* qn = nullptr, uint32_t* dst = nullptr) {
+    for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
+        const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
+        for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
+            const uint32_t a = pstart[k] > lo ? pstart[k] : lo;
+            const uint32_t z = pstart[k + 1] < hi ? pstart[k + 1] : hi;
+            for (uint32_t x = a; x < z; x++) owner[x - lo] = (uint16_t)k;
+        }
+        __syncthreads();
+        uint4 v[FX_DEPTH];
+#pragma unroll
+        for (int j = 0; j < FX_DEPTH; j++) {
+            const uint32_t x = lo + j * TM_NT + threadIdx.x;
+            v[j] = make_uint4(~0u, ~0u, ~0u, ~0u);
+            if (x < hi) {
+                const uint32_t k = owner[x - lo];
+                v[j] = ent[plo[k] + (x - pstart[k])];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < FX_DEPTH; j++) {
+            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst);
+            else fx_count_block(cnt, v[j]);
+        }
+        __syncthreads();
+    }
+}
+
+// Every counter byte >= thr (1..127) of cnt[0 .. nbytes), nbytes a multiple
+// of 16: f(index).  Counters never exceed 32, so byte + (128 - thr) sets bit
+// 7 exactly when byte >= thr, without carries between bytes.
+template <typename F>
+__device__ __forceinline__ void fx_qualify(const uint32_t* cnt, uint32_t nbytes, uint32_t thr, F f) {
+    const uint32_t add = 0x01010101u * (128u - thr);
+    const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
+    for (uint32_t i = threadIdx.x; i < nbytes / 16; i += TM_NT) {
+        const uint4 x = c4[i];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            for (uint32_t m = (w[q] + add) & 0x80808080u; m; m &= m - 1) f(16 * i + 4 * q + ((__ffs(m) - 1) >> 3));
+        }
+    }
+}
+
+// The counter bytes >= thr of cnt[0 .. nbytes) as slots base + index,
+// appended to dst at *qn.  A first sweep counts each wave's hits (one LDS
+// atomic per wave reserves its range), a second writes them, ranked within
+// the wave by ballot bit counts -- no per-iteration scans or atomics.
+__device__ __forceinline__ void fx_collect(const uint32_t* cnt, uint32_t nbytes, uint32_t thr, uint32_t base,
+                                           int32_t* qn, uint32_t* dst) {
+    const uint32_t add = 0x01010101u * (128u - thr);
+    const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
+    const uint32_t n16 = nbytes / 16;
+    uint32_t mine = 0;
+    for (uint32_t i = threadIdx.x; i < n16; i += TM_NT) {
+        const uint4 x = c4[i];
+        mine += __popc((x.x + add) & 0x80808080u) + __popc((x.y + add) & 0x80808080u) +
+                __popc((x.z + add) & 0x80808080u) + __popc((x.w + add) & 0x80808080u);
+    }
+    const uint32_t wtot = wave_sum_u32(mine);
+    if (wtot == 0) return;  // wave-uniform
+    uint32_t pos = 0;
+    if (lane_id() == 0) pos = (uint32_t)atomicAdd(qn, (int32_t)wtot);
+    pos = __shfl(pos, 0, 64);
+    for (uint32_t i0 = 0; i0 < n16; i0 += TM_NT) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint32_t m[4] = {0u, 0u, 0u, 0u};
+        if (i < n16) {
+            const uint4 x = c4[i];
+            m[0] = (x.x + add) & 0x80808080u;
+            m[1] = (x.y + add) & 0x80808080u;
+            m[2] = (x.z + add) & 0x80808080u;
+            m[3] = (x.w + add) & 0x80808080u;
+        }
+        for (;;) {
+            const int q = m[0] ? 0 : m[1] ? 1 : m[2] ? 2 : m[3] ? 3 : -1;
+            const uint64_t bal = __ballot(q >= 0);
+            if (!bal) break;
+            if (q >= 0) {
+                const uint32_t x = q == 0 ? m[0] : q == 1 ? m[1] : q == 2 ? m[2] : m[3];
+                dst[pos + ballot_rank(bal)] = base + 16 * i + 4 * q + ((__ffs(x) - 1) >> 3);
+                const uint32_t y = x & (x - 1);
+                if (q == 0) m[0] = y; else if (q == 1) m[1] = y; else if (q == 2) m[2] = y; else m[3] = y;
+            }
+            pos += (uint32_t)__popcll(bal);
+        }
+    }
+}
+
+// zero n 16-byte quads of LDS
+__device__ __forceinline__ void wg_clear4(uint32_t* p, uint32_t nquads) {
+    uint4* p4 = reinterpret_cast<uint4*>(p);
+    for (uint32_t i = threadIdx.x; i < nquads; i += TM_NT) p4[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// learning-off form: forward propagation over the frozen cell->segment index
+// (what Cells4's _outSynapses does).  Pass 0 counts CONNECTED active
+// synapses of the predictive-capable segments (pid lists; counter >=
+// activationThreshold predicts the segment's cell); then, per window of the
+// slot space, all active synapses of every segment (counter >= thr: the
+// segment qualifies for the confidence sum).
 __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
@@ -332,27 +464,47 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4);
     uint32_t* pstart = t.U + W / 4 + (mac + 1) / 2;
     uint32_t* plo = pstart + mac + 1;
+    uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
     const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
     const uint32_t na = nact < mac ? nact : mac;
     const uint32_t hwm = sh->hwm;
     STAMP(t, SB_LIST);
     COUNT(t, SC_NACT, na);
     const uint32_t nwin = (uint32_t)c.fx_nwin;
-    const uint32_t per = (na + TM_NT - 1) / TM_NT;
+    const uint32_t nw = (hwm + W - 1) / W;
+    const bool pid_ok = t.np <= (uint32_t)c.fx_pcap;
+    const uint32_t per = (na + TM_NT - 1) / TM_NT;  // <= FX_MAXPER (na <= 64 x 32)
     const uint32_t k0 = threadIdx.x * per;
-    const uint32_t lane = lane_id();
     uint32_t nblk = 0;
-    for (uint32_t w = 0; w * W < hwm; w++) {
-        uint32_t lsum = 0;
-        for (uint32_t j = 0; j < per; j++) {
+    // block ranges of this thread's cells in pass w, loaded one pass ahead
+    uint32_t olo[FX_MAXPER], ohi[FX_MAXPER];
+    auto load_offsets = [&](int w) {
+#pragma unroll
+        for (uint32_t j = 0; j < FX_MAXPER; j++) {
             const uint32_t k = k0 + j;
-            if (k >= na) break;
-            const uint32_t* o = t.fxoff + (size_t)cells[k] * nwin + w;
-            const uint32_t lo = o[0], n = o[1] - lo;
-            plo[k] = lo;
-            pstart[k] = n;
-            lsum += n;
+            if (j < per && k < na) {
+                const size_t idx =
+                    w < 0 ? (size_t)c.ncells * nwin + cells[k] : (size_t)cells[k] * nwin + (uint32_t)w;
+                olo[j] = t.fxoff[idx];
+                ohi[j] = t.fxoff[idx + 1];
+            }
         }
+    };
+    const int w_first = (pid_ok && t.np > 0) ? -1 : 0;
+    load_offsets(w_first);
+    for (int w = w_first; w < (int)nw; w++) {
+        // list of (active cell k, pass w): block range [fxoff[idx], fxoff[idx + 1])
+        uint32_t lsum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < FX_MAXPER; j++) {
+            const uint32_t k = k0 + j;
+            if (j < per && k < na) {
+                plo[k] = olo[j];
+                pstart[k] = ohi[j] - olo[j];
+                lsum += ohi[j] - olo[j];
+            }
+        }
+        if (w + 1 < (int)nw) load_offsets(w + 1);
         uint32_t B;
         uint32_t pos = wg_excl_scan(sh, lsum, &B);
         for (uint32_t j = 0; j < per; j++) {
@@ -364,79 +516,56 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         }
         if (threadIdx.x == 0) pstart[na] = B;
         nblk += B;
-        wg_clear(cnt, (int)(W / 4));
+        const uint32_t nbytes = w < 0 ? (t.np + 15u) & ~15u : W;
+        wg_clear4(cnt, nbytes / 16);
         __syncthreads();
         STAMP(t, SB_WINPRE);
         COUNT(t, SC_WIN, 1);
         COUNT(t, SC_BLK, B);
-        const uint32_t pw = (B + TM_NWAVES - 1) / TM_NWAVES;
-        const uint32_t b0 = wave_id() * pw;
-        const uint32_t b1 = b0 + pw < B ? b0 + pw : B;
-        if (b0 < b1) {
-            uint32_t kc = fx_find(pstart, 0, na, b0);
-            for (uint32_t base = b0; base < b1; base += 128) {
-                const uint32_t ba = base + lane, bb = base + 64 + lane;
-                const uint4 pad = make_uint4(~0u, ~0u, ~0u, ~0u);
-                uint4 va = pad, vb = pad;
-                uint32_t ka = kc, kb = kc;
-                if (ba < b1) {
-                    ka = fx_find(pstart, kc, na, ba);
-                    va = t.fxent[plo[ka] + (ba - pstart[ka])];
-                }
-                if (bb < b1) {
-                    kb = fx_find(pstart, ka, na, bb);
-                    vb = t.fxent[plo[kb] + (bb - pstart[kb])];
-                }
-                kc = wave_max_u32(kb > ka ? kb : ka);
-                fx_count_block(cnt, va);
-                fx_count_block(cnt, vb);
-            }
-        }
-        __syncthreads();
+        if (w < 0) fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner);
+        else fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, (uint32_t)thr, (uint32_t)w * W, &sh->qn, t.q1);
         STAMP(t, SB_STREAM);
-        for (uint32_t i = threadIdx.x; i < W / 4; i += TM_NT) {
-            uint32_t x = cnt[i];
-            if (!x) continue;
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                if (((x >> (8 * b)) & 0xFFu) >= (uint32_t)thr) {
-                    int q = atomicAdd(&t.sh->qn, 1);
-                    t.q1[q] = w * W + 4 * i + b;
+        if (w < 0) {
+            // pid counter >= activationThreshold: the segment's cell is predicted
+            const uint32_t np = t.np;
+            uint32_t* infP = t.infP;
+            const uint16_t* pcell = t.fxpcell;
+            fx_qualify(cnt, nbytes, (uint32_t)c.act_thr, [&](uint32_t pid) {
+                if (pid < np) {
+                    const uint32_t cell = pcell[pid];
+                    atomicOr(&infP[cell >> 5], 1u << (cell & 31));
                 }
-            }
+            });
+            __syncthreads();
         }
-        __syncthreads();
         STAMP(t, SB_QSCAN);
     }
-    // out-list blocks + the two block offsets of every (active cell, window)
-    const uint32_t nw = (hwm + W - 1) / W;
-    if (threadIdx.x == 0) sh->bytes += 16ull * nblk + 8ull * na * nw;
+    // out-list blocks + the two block offsets of every (active cell, pass)
+    if (threadIdx.x == 0) sh->bytes += 16ull * nblk + 8ull * na * (nw + (pid_ok && t.np > 0 ? 1u : 0u));
 }
 
-// Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
-// NuPIC order, normalisation.  Returns numPredictedCols (uniform).
-__device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
+// Pass 1 of _inferPhase2 over the qn qualifying segments in t.q1: the
+// predicted cells (rows path; the frozen pid path predicted them while
+// counting), the dutyCycle() each contributes, emit(k, slot, cell, dc).
+// Returns this thread's algorithmic bytes.
+template <bool FROZEN, typename F>
+__device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
-    const int K = c.K;
-    const uint32_t qn = (uint32_t)sh->qn;
-    uint32_t* colcnt = t.U;
-    uint16_t* nzcol = reinterpret_cast<uint16_t*>(t.U + c.ncol);
-    uint32_t* nzstart = t.U + c.ncol + (c.ncol + 1) / 2;
-    // qualifying segments (<= q_lds of them): key, dutyCycle, column; and
-    // the same sorted by column bucket
-    const uint32_t ql = (uint32_t)c.q_lds;
-    uint32_t* qkey = nzstart + c.ncol + 1;
-    float* qdc = reinterpret_cast<float*>(qkey + ql);
-    uint32_t* skey = qkey + 2 * ql;
-    float* sdc = reinterpret_cast<float*>(qkey + 3 * ql);
-    uint16_t* qcol = reinterpret_cast<uint16_t*>(qkey + 4 * ql);
-    const bool in_lds = qn <= ql;
-    wg_clear(colcnt, c.ncol);
-    __syncthreads();
-    // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
     uint32_t nb = 0;
-    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+    const bool fx_pid = FROZEN && t.np <= (uint32_t)c.fx_pcap;
+    for (uint32_t k = threadIdx.x; k < qn && fx_pid; k += TM_NT) {
+        // frozen index: cell and the (frozen-iteration) dutyCycle of the
+        // segment.  The dutyCycle() state update is a store of the value it
+        // returns.
+        const uint32_t slot = t.q1[k];
+        const uint2 rec = t.fxrec[slot];
+        t.duty[(size_t)slot * 3 + 1] = rec.y;
+        t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
+        nb += 8u + 8u;
+        emit(k, slot, rec.x, __uint_as_float(rec.y));
+    }
+    for (uint32_t k = threadIdx.x; k < qn && !fx_pid; k += TM_NT) {
         uint32_t slot = t.q1[k];
         uint32_t m = t.meta[slot];
         uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
@@ -457,7 +586,121 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
             }
         }
         if (n >= (uint32_t)c.act_thr) atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
-        const float dc = seg_dc_update(t.duty, slot, sh->lrn_iter, false);
+        emit(k, slot, cell, seg_dc_update(t.duty, slot, sh->lrn_iter, false));
+    }
+    return nb;
+}
+
+// numPredictedCols: columns with a predicted cell (uniform; has barriers)
+__device__ __forceinline__ uint32_t count_predicted_cols(Tm& t) {
+    const DevCfg& c = t.c;
+    uint32_t n = 0;
+    for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
+        if (bm_field(t.infP, (uint32_t)col * c.K, c.K)) n++;
+    return wg_sum(t.sh, n);
+}
+
+// Tail of _inferPhase2 for qn <= q_lds (<= 1024) qualifying segments: the
+// keys col:12 | cellInColumn:5 | slot:27 | k:10 are bitonic-sorted in LDS,
+// each column's confidence is summed over its run in that order -- NuPIC's
+// (column, cell, segment) order -- and the normaliser is folded over the
+// columns in ascending order, so the float32 results are bit-identical to
+// the oracle.  Returns numPredictedCols.
+template <bool FROZEN>
+__device__ __forceinline__ uint32_t phase2_finish_sorted(Tm& t, uint32_t qn) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int K = c.K;
+    const uint32_t ql = (uint32_t)c.q_lds;
+    uint64_t* qk = reinterpret_cast<uint64_t*>(t.U);     // [ql] keys, sorted in place
+    float* qd = reinterpret_cast<float*>(t.U + 2 * ql);  // [ql] dutyCycle by pass-1 index k
+    float* rs = reinterpret_cast<float*>(t.U + 3 * ql);  // [ql] run sums at run heads, -1 elsewhere
+    uint32_t nb = phase2_pass1<FROZEN>(t, qn, [&](uint32_t k, uint32_t slot, uint32_t cell, float dc) {
+        const uint32_t col = col_of(c, cell);
+        qk[k] = ((uint64_t)col << 42) | ((uint64_t)(cell - col * K) << 37) | ((uint64_t)slot << 10) | k;
+        qd[k] = dc;
+    });
+    uint32_t n2 = 1;  // pad to a power of two with +inf keys
+    while (n2 < qn) n2 <<= 1;
+    for (uint32_t k = qn + threadIdx.x; k < n2; k += TM_NT) qk[k] = ~0ull;
+    nb = wg_sum(sh, nb);
+    if (threadIdx.x == 0) sh->bytes += nb;
+    STAMP(t, SB_FIN1);
+    COUNT(t, SC_QN, qn);
+    COUNT(t, SC_P2, 1);
+    for (uint32_t size = 2; size <= n2; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2 / 2; i += TM_NT) {
+                const uint32_t lo = 2 * i - (i & (stride - 1));
+                const uint32_t hi = lo + stride;
+                const uint64_t a = qk[lo], b = qk[hi];
+                if ((a > b) == ((lo & size) == 0)) {
+                    qk[lo] = b;
+                    qk[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    STAMP(t, SB_SORT);
+    // run heads sum their column in order; -1 marks the other entries
+    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+        const uint32_t col = (uint32_t)(qk[k] >> 42);
+        if (k > 0 && (uint32_t)(qk[k - 1] >> 42) == col) {
+            rs[k] = -1.0f;
+            continue;
+        }
+        float sum = 0.0f;
+        for (uint32_t j = k; j < qn && (uint32_t)(qk[j] >> 42) == col; j++) sum += qd[qk[j] & 1023u];
+        t.colconf[col] = sum;
+        rs[k] = sum;
+    }
+    __syncthreads();
+    STAMP(t, SB_SUMS);
+    // normaliser: sequential sum over the nonzero columns, ascending (the
+    // -1 markers of non-head entries add +0.0f, which leaves the sum exact)
+    if (threadIdx.x == 0) {
+        float tot = 0.0f;
+#pragma unroll 8
+        for (uint32_t k = 0; k < qn; k++) tot += fmaxf(rs[k], 0.0f);
+        sh->tf[0] = tot;
+    }
+    __syncthreads();
+    const float tot = sh->tf[0];
+    if (tot > 0.0f)
+        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT)
+            if (rs[k] >= 0.0f) t.colconf[(uint32_t)(qk[k] >> 42)] = rs[k] / tot;
+    const uint32_t npcol = count_predicted_cols(t);
+    STAMP(t, SB_FIN2);
+    return npcol;
+}
+
+// Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
+// NuPIC order, normalisation.  Returns numPredictedCols (uniform).
+template <bool FROZEN>
+__device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
+    if (t.c.fin_sorted && (uint32_t)t.sh->qn <= (uint32_t)t.c.q_lds)
+        return phase2_finish_sorted<FROZEN>(t, (uint32_t)t.sh->qn);
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int K = c.K;
+    const uint32_t qn = (uint32_t)sh->qn;
+    uint32_t* colcnt = t.U;
+    uint16_t* nzcol = reinterpret_cast<uint16_t*>(t.U + c.ncol);
+    uint32_t* nzstart = t.U + c.ncol + (c.ncol + 1) / 2;
+    // qualifying segments (<= q_lds of them): key, dutyCycle, column; and
+    // the same sorted by column bucket
+    const uint32_t ql = (uint32_t)c.q_lds;
+    uint32_t* qkey = nzstart + c.ncol + 1;
+    float* qdc = reinterpret_cast<float*>(qkey + ql);
+    uint32_t* skey = qkey + 2 * ql;
+    float* sdc = reinterpret_cast<float*>(qkey + 3 * ql);
+    uint16_t* qcol = reinterpret_cast<uint16_t*>(qkey + 4 * ql);
+    const bool in_lds = qn <= ql;
+    wg_clear(colcnt, c.ncol);
+    __syncthreads();
+    // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
+    uint32_t nb = phase2_pass1<FROZEN>(t, qn, [&](uint32_t k, uint32_t slot, uint32_t cell, float dc) {
         const uint32_t col = col_of(c, cell);
         atomicAdd(&colcnt[col], 1u);
         if (in_lds) {
@@ -465,7 +708,7 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
             qdc[k] = dc;
             qcol[k] = (uint16_t)col;
         }
-    }
+    });
     nb = wg_sum(sh, nb);
     if (threadIdx.x == 0) sh->bytes += nb;
     STAMP(t, SB_FIN1);
@@ -548,18 +791,12 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
         if (bm_field(t.infP, col * K, K)) npcol++;
     }
     npcol = wg_sum(sh, npcol);
-    // total in nonzero-column order (ascending), sequentially as NuPIC sums
-    // it: wave 0 stages 64 columns per VGPR and folds them lane by lane
-    if (wave_id() == 0) {
+    // total in nonzero-column order (ascending), sequentially as NuPIC sums it
+    if (threadIdx.x == 0) {
         float tot = 0.0f;
-        for (uint32_t base = 0; base < tnz; base += 64) {
-            const uint32_t i = base + lane_id();
-            const float v = i < tnz ? t.colconf[nzcol[i]] : 0.0f;
-            const uint32_t m = tnz - base < 64 ? tnz - base : 64;
-            for (uint32_t j = 0; j < m; j++)
-                tot += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-        }
-        if (lane_id() == 0) sh->tf[0] = tot;
+#pragma unroll 8
+        for (uint32_t i = 0; i < tnz; i++) tot += t.colconf[nzcol[i]];
+        sh->tf[0] = tot;
     }
     __syncthreads();
     float tot = sh->tf[0];
@@ -585,7 +822,7 @@ __device__ __forceinline__ bool infer_phase2(Tm& t) {
     if (FROZEN) collect_frozen(t, t.c.act_thr);
     else collect_scan(t, t.infA, t.c.act_thr);
     __syncthreads();
-    uint32_t npc = phase2_finish(t);
+    uint32_t npc = phase2_finish<FROZEN>(t);
     return (double)npc >= 0.5 * sh->avg_dens;
 }
 
@@ -1364,10 +1601,11 @@ __device__ __forceinline__ void compact_pool(Tm& t) {
 }
 
 // ---------------------------------------------------------------------------
+// One BacktrackingTM.compute + raw anomaly of stream s by the calling
+// workgroup (TM_NT threads), LDS at `lds` (tm_layout).
 template <bool LEARN, bool FROZEN>
-__global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBufs sp, float* scores, int keep_prev) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int s = blockIdx.x;
+__device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores,
+                                             int keep_prev, int s, uint8_t* lds) {
     const TmLayout L = tm_layout(c, LEARN, FROZEN);
     Tm t;
     t.c = c;
@@ -1397,17 +1635,26 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
     t.q1 = b.scr_q + (size_t)s * sc;
     t.q2 = b.scr_q2 + (size_t)s * sc;
     if (FROZEN) {
-        t.fxoff = b.fx_off + (size_t)s * ((size_t)c.ncells * c.fx_nwin + 1);
+        t.fxoff = b.fx_off + (size_t)s * (size_t)c.fx_noff;
         t.fxent = b.fx_ent + b.fx_base[s];
+        t.fxrec = b.fx_rec + (size_t)s * sc;
+        t.fxpcell = b.fx_pcell + (size_t)s * c.fx_pcap;
+        t.np = b.fx_np[s];
     } else {
         t.fxoff = nullptr;
         t.fxent = nullptr;
+        t.fxrec = nullptr;
+        t.fxpcell = nullptr;
+        t.np = 0;
     }
-#ifdef HTM_STAMPS
-    for (int k = 0; k < HTM_NSTAMP; k++) t.acc[k] = t.cnt[k] = 0;
-    t.last = __builtin_amdgcn_s_memtime();
-#endif
     TmSh* sh = t.sh;
+#ifdef HTM_STAMPS
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < HTM_NSTAMP; k++) sh->st_acc[k] = sh->st_cnt[k] = 0;
+        sh->st_last = __builtin_amdgcn_s_memtime();
+        sh->st_start = sh->st_last;
+    }
+#endif
     htm_tm_header* hdr = b.hdr + s;
     uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
     float* gconf = b.colconf + (size_t)s * c.ncol;
@@ -1560,14 +1807,64 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
     __syncthreads();
     STAMP(t, SB_WB);
     COUNT(t, SC_STEPS, 1);
+    if (threadIdx.x == 0) {
+        uint64_t x = (sh->st_last - sh->st_start) >> 16;
+        int hb = 0;
+        while (x && hb < 8) { hb++; x >>= 1; }
+        sh->st_cnt[SC_HIST + hb] += 1;
+    }
     if (threadIdx.x == 0 && b.dbg) {
         uint64_t* d = b.dbg + (size_t)s * 32;
         for (int k = 0; k < HTM_NSTAMP; k++) {
-            d[k] += t.acc[k];
-            d[16 + k] += t.cnt[k];
+            d[k] += sh->st_acc[k];
+            d[16 + k] += sh->st_cnt[k];
         }
     }
 #endif
+}
+
+template <bool LEARN, bool FROZEN>
+__global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBufs sp, float* scores, int keep_prev) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    tm_step_body<LEARN, FROZEN>(c, b, sp, scores, keep_prev, blockIdx.x, lds);
+}
+
+// Fused network.run(1) x n_steps: each workgroup steps its stream through
+// encoder -> SP -> TM -> anomaly for n_steps consecutive records, so a
+// stream never waits for the others between steps (streams are
+// independent; every stream's result is the one per-step launches give).
+// The SP's LDS aliases the TM union region, which is free between steps.
+template <bool LEARN, bool FROZEN>
+__global__ __launch_bounds__(TM_NT) void htm_run_kernel(DevCfg c, TmBufs b, SpBufs sp, const double* values,
+                                                        float* scores, int n_steps, int sp_learn, int keep_prev,
+                                                        int keep_overlaps) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int s = blockIdx.x;
+    SpShared& ssh = *reinterpret_cast<SpShared*>(lds + tm_layout(c, LEARN, FROZEN).off_U);
+    for (int k = 0; k < n_steps; k++) {
+        const double* v = values + (size_t)k * c.n_streams * c.n_fields;
+        if (sp_learn) sp_step_body<true>(c, sp, v, s, ssh, keep_overlaps);
+        else sp_step_body<false>(c, sp, v, s, ssh, keep_overlaps);
+        __syncthreads();
+        tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds);
+        __syncthreads();
+    }
+}
+
+int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
+                   int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
+                   hipStream_t st) {
+    size_t lds = tm_step_lds_bytes(c, tm_learn, frozen);
+    if (tm_learn)
+        hipLaunchKernelGGL((htm_run_kernel<true, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, values, scores,
+                           n_steps, sp_learn, keep_prev, keep_overlaps);
+    else if (frozen)
+        hipLaunchKernelGGL((htm_run_kernel<false, true>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, values, scores,
+                           n_steps, sp_learn, keep_prev, keep_overlaps);
+    else
+        hipLaunchKernelGGL((htm_run_kernel<false, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, values, scores,
+                           n_steps, sp_learn, keep_prev, keep_overlaps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen, int n,
@@ -1624,28 +1921,85 @@ int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
-// Frozen forward index build.  counts[s] = total entries of stream s.
-// fx_off[s] doubles as the per-(cell, window) counter array.
+// Frozen forward index build.  counts[s] = total blocks of stream s.
+// fx_off[s] doubles as the per-list entry counter array; scr_q2[s] holds the
+// pid of each slot (~0u: not predictive-capable) between count and fill.
+
+// Segment::dutyCycle(it, active=false) without the state update: the value
+// the frozen phase 2 reads for the segment (seg_dc_update's arithmetic).
+__device__ __forceinline__ float seg_dc_peek(const uint32_t* duty, uint32_t slot, uint32_t it) {
+    const uint32_t* d = duty + (size_t)slot * 3;
+    if (it <= kDcTier[1]) return (float)d[0] / (float)it;
+    const uint32_t age = it - d[2];
+    const float last = __uint_as_float(d[1]);
+    if (age == 0) return last;
+    float alpha = 0.0f;
+    for (int t = 8; t > 0; t--) {
+        if (it > kDcTier[t]) { alpha = kDcAlpha[t]; break; }
+    }
+    return pow_det((float)(1.0 - (double)alpha), age) * last;
+}
+
 __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
     const int s = blockIdx.x;
     const size_t sc = (size_t)c.seg_cap;
     const uint32_t* meta = b.seg_meta + (size_t)s * sc;
     const uint16_t* src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
-    const size_t noff = (size_t)c.ncells * c.fx_nwin + 1;
+    const uint32_t* conn = b.seg_conn + (size_t)s * sc;
+    const size_t noff = (size_t)c.fx_noff;
+    const size_t p0 = (size_t)c.ncells * c.fx_nwin;  // first pid-list counter
     uint32_t* off = b.fx_off + (size_t)s * noff;
+    uint32_t* pid = b.scr_q2 + (size_t)s * sc;
+    uint16_t* pcell = b.fx_pcell + (size_t)s * c.fx_pcap;
     const uint32_t hwm = b.hdr[s].seg_hwm;
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t tot;
     for (size_t i = threadIdx.x; i < noff; i += blockDim.x) off[i] = 0u;
     __syncthreads();
-    for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
-        uint32_t m = meta[slot];
-        if (!meta_live(m)) continue;
-        uint32_t nsyn = meta_nsyn(m), w = slot / (uint32_t)c.fx_win;
-        for (uint32_t j = 0; j < nsyn; j++) atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+    // window-list entry counts; predictive-capable flags over a contiguous
+    // chunk of slots per thread (pids are dense in slot order)
+    const uint32_t sper = (hwm + blockDim.x - 1) / blockDim.x;
+    const uint32_t s0 = threadIdx.x * sper, s1 = s0 + sper < hwm ? s0 + sper : hwm;
+    uint32_t ncap = 0;
+    for (uint32_t slot = s0; slot < s1; slot++) {
+        const uint32_t m = meta[slot];
+        uint32_t p = ~0u;
+        if (meta_live(m)) {
+            const uint32_t nsyn = meta_nsyn(m), w = slot / (uint32_t)c.fx_win;
+            for (uint32_t j = 0; j < nsyn; j++)
+                atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+            const uint32_t cm = conn[slot] & (nsyn >= 32 ? ~0u : ((1u << nsyn) - 1u));
+            if (__popc(cm) >= (uint32_t)c.act_thr) {
+                p = 0u;
+                ncap++;
+            }
+        }
+        pid[slot] = p;
+    }
+    part[threadIdx.x] = ncap;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < (int)blockDim.x; k++) { uint32_t v = part[k]; part[k] = run; run += v; }
+        tot = run;
+        b.fx_np[s] = run;
+    }
+    __syncthreads();
+    const uint32_t np = tot;
+    if (np <= (uint32_t)c.fx_pcap) {
+        uint32_t next = part[threadIdx.x];
+        for (uint32_t slot = s0; slot < s1; slot++) {
+            if (pid[slot] == ~0u) continue;
+            const uint32_t m = meta[slot], nsyn = meta_nsyn(m), cm = conn[slot];
+            pid[slot] = next;
+            pcell[next] = (uint16_t)meta_cell(m);
+            next++;
+            for (uint32_t j = 0; j < nsyn; j++)
+                if ((cm >> j) & 1u) atomicAdd(&off[p0 + src[(size_t)slot * HTM_MAXSYN + j]], 1u);
+        }
     }
     __syncthreads();
     // entries -> 16-byte blocks of 8, then exclusive scan (chunked per thread)
-    __shared__ uint32_t part[256];
-    __shared__ uint32_t tot;
     const size_t per = (noff + blockDim.x - 1) / blockDim.x;
     const size_t i0 = threadIdx.x * per;
     uint32_t sum = 0;
@@ -1654,6 +2008,7 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
         off[i0 + k] = nb;
         sum += nb;
     }
+    __syncthreads();
     part[threadIdx.x] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1676,18 +2031,25 @@ int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// fill: per-(cell, window) entry cursors in scr_cur; fx_ent was set to
-// 0xFF.. by the host, so the tail of each list's last block stays padding
+// fill: per-list entry cursors in scr_cur; fx_ent was set to 0xFF.. by the
+// host, so the tail of each list's last block stays padding
 __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
     const int s = blockIdx.x;
     const size_t sc = (size_t)c.seg_cap;
     const uint32_t* meta = b.seg_meta + (size_t)s * sc;
     const uint16_t* src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
-    const size_t noff = (size_t)c.ncells * c.fx_nwin + 1;
+    const uint32_t* conn = b.seg_conn + (size_t)s * sc;
+    const uint32_t* duty = b.seg_duty + (size_t)s * sc * 3;
+    const uint32_t* pid = b.scr_q2 + (size_t)s * sc;
+    const size_t noff = (size_t)c.fx_noff;
+    const size_t p0 = (size_t)c.ncells * c.fx_nwin;
     const uint32_t* off = b.fx_off + (size_t)s * noff;
-    uint32_t* cur = b.scr_cur + (size_t)s * ((size_t)c.ncells * c.fx_nwin);
+    uint32_t* cur = b.scr_cur + (size_t)s * noff;
     uint16_t* ent = reinterpret_cast<uint16_t*>(b.fx_ent + b.fx_base[s]);
+    uint2* rec = b.fx_rec + (size_t)s * sc;
     const uint32_t hwm = b.hdr[s].seg_hwm;
+    const uint32_t it = b.hdr[s].lrn_iter;
+    const bool pid_ok = b.fx_np[s] <= (uint32_t)c.fx_pcap;
     const uint32_t W = (uint32_t)c.fx_win;
     for (size_t i = threadIdx.x; i + 1 < noff; i += blockDim.x) cur[i] = off[i] * 8u;
     __syncthreads();
@@ -1698,6 +2060,16 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
         for (uint32_t j = 0; j < nsyn; j++) {
             uint32_t pos = atomicAdd(&cur[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
             ent[pos] = (uint16_t)(slot - w * W);
+        }
+        rec[slot] = make_uint2(meta_cell(m), __float_as_uint(seg_dc_peek(duty, slot, it)));
+        const uint32_t p = pid[slot];
+        if (pid_ok && p != ~0u) {
+            const uint32_t cm = conn[slot];
+            for (uint32_t j = 0; j < nsyn; j++) {
+                if (!((cm >> j) & 1u)) continue;
+                uint32_t pos = atomicAdd(&cur[p0 + src[(size_t)slot * HTM_MAXSYN + j]], 1u);
+                ent[pos] = (uint16_t)p;
+            }
         }
     }
 }
@@ -1711,8 +2083,17 @@ int tm_configure_lds(const DevCfg& c) {
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
     hipError_t e2 = hipFuncSetAttribute((const void*)tm_step_kernel<false, false>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
+    hipError_t e3 = hipFuncSetAttribute((const void*)htm_run_kernel<true, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b0);
+    hipError_t e4 = hipFuncSetAttribute((const void*)htm_run_kernel<false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
+    hipError_t e5 = hipFuncSetAttribute((const void*)htm_run_kernel<false, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
     (void)hipGetLastError();
-    return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess) ? 0 : -1;
+    return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess && e4 == hipSuccess &&
+            e5 == hipSuccess)
+               ? 0
+               : -1;
 }
 
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {

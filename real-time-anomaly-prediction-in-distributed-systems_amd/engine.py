@@ -168,9 +168,18 @@ class HTMEngine:
         self.set_option(_lib.OPT_PROFILE, int(on))
 
     def profile_read(self) -> dict:
+        """{sp_ms, tm_ms (fused launches: SP+TM), steps covered, launches}."""
         out = (ctypes.c_double * 4)()
         check(self._L.htm_profile_read(self.h, out))
-        return dict(sp_ms=out[0], tm_ms=out[1], steps=int(out[2]))
+        return dict(sp_ms=out[0], tm_ms=out[1], steps=int(out[2]), launches=int(out[3]))
+
+    def use_fused(self, on: bool):
+        """One fused SP+TM kernel per step / per htm_run chunk (default on)."""
+        self.set_option(_lib.OPT_FUSED, int(on))
+
+    def set_run_chunk(self, steps: int):
+        """Steps per fused htm_run launch."""
+        self.set_option(_lib.OPT_RUN_CHUNK, int(steps))
 
     def counters(self) -> dict:
         out = (ctypes.c_uint64 * 8)()
@@ -184,10 +193,11 @@ class HTMEngine:
         out = (ctypes.c_uint64 * 32)()
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
-                 "scan"]
+                 "scan", "sort", "sums"]
         cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
         return dict(cycles={k: int(out[i]) for i, k in enumerate(names)},
-                    counts={k: int(out[16 + i]) for i, k in enumerate(cnames)})
+                    counts={k: int(out[16 + i]) for i, k in enumerate(cnames)},
+                    step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[23 + b]) for b in range(9)})
 
     def frozen_index_valid(self) -> bool:
         return bool(self._L.htm_frozen_index_valid(self.h))

@@ -38,5 +38,6 @@ tot = sum(st["cycles"].values())
 out = {"streams": N, "steps": T, "tm_ms_per_launch": prof["tm_ms"] / prof["steps"],
        "cycles_per_stream_step": {k: round(v / steps, 1) for k, v in st["cycles"].items()},
        "total_cycles_per_stream_step": round(tot / steps, 1),
-       "counts_per_stream_step": {k: round(v / steps, 3) for k, v in st["counts"].items()}}
+       "counts_per_stream_step": {k: round(v / steps, 3) for k, v in st["counts"].items()},
+       "step_cycle_hist": st["step_cycle_hist"]}
 print(json.dumps(out, indent=1))
