@@ -8,9 +8,14 @@ from tests/golden/model1_traces.npz).  Inputs are synthetic, resident in HBM:
     cpu[s,t] = clip(trace[(t + 97 s) mod 2324] + d[s,t], 0, 100)
 trace = TestingData.txt cpu column, d uniform integer in {-2..2} from
 numpy PCG64(seed=724).  A step = one network.run(1) of every stream
-(encoder -> SP -> TM -> raw anomaly).  N>1 GPUs: weak scaling, streams
-sharded by rank, per-step RCCL gather of the anomaly scores to rank 0
-(the SLO alerting path).
+(encoder -> SP -> TM -> raw anomaly).  `value` times the K steps as htm_run
+replay chunks (the reference's offline replay of recorded metrics,
+ModelTesting.py over TestingData.txt, batched: each stream steps through a
+chunk without waiting for the others); the same engine is then also timed
+in lockstep (one htm_step per step, every stream waits for the slowest) and
+reported as `lockstep`.  N>1 GPUs: weak scaling, streams sharded by rank,
+RCCL gather of every step's anomaly scores to rank 0 (the SLO alerting
+path), overlapped with the next chunk.
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S]
 """
@@ -86,16 +91,36 @@ def cpu_baseline(trace, train_vals, n_total, target_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2324)
-    ap.add_argument("--warmup", type=int, default=64)
-    ap.add_argument("--streams", type=int, default=1024, help="streams per GPU")
-    ap.add_argument("--seg-capacity", type=int, default=72 * 1024)
+    ap.add_argument("--config", type=int, choices=[2, 3], default=2,
+                    help="2 (default, the metric's config): trained Model-1 streams, learning off; "
+                         "3: fresh streams (seed 2045 + s), SP+TM learning on, 256 steps")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: 2324, config 3: 240)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config 2: 64, config 3: 16)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="streams per GPU (config 2: 1024; config 3: 40960 -- 65,536 x 256 learning steps "
+                         "needs ~380 GB of float32 state, more than one MI355X holds; see DESIGN.md)")
+    ap.add_argument("--seg-capacity", type=int, default=None, help="segment slots per stream")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
-    ap.add_argument("--mode", choices=["step", "run"], default="step",
-                    help="step: one htm_step (network.run(1) of every stream) per step, lockstep; "
-                         "run: the K steps as htm_run replay chunks (each stream runs ahead independently)")
+    ap.add_argument("--mode", choices=["step", "run"], default="run",
+                    help="run (default): the K steps as htm_run replay chunks -- every stream steps through "
+                         "the chunk without waiting for the others (the reference's offline replay of "
+                         "recorded metrics, batched); step: one lockstep htm_step per step")
+    ap.add_argument("--chunk", type=int, default=256, help="steps per htm_run call in run mode")
+    ap.add_argument("--lockstep-steps", type=int, default=256,
+                    help="after the timed region, also time this many lockstep htm_step steps (0: skip)")
     args = ap.parse_args()
+    c3 = args.config == 3
+    if args.steps is None:
+        args.steps = 240 if c3 else 2324
+    if args.warmup is None:
+        args.warmup = 16 if c3 else 64
+    if args.streams is None:
+        args.streams = 40960 if c3 else 1024
+    if args.seg_capacity is None:
+        args.seg_capacity = 10240 if c3 else 72 * 1024
+    if c3:
+        args.lockstep_steps = 0
 
     import torch
     import torch.distributed as dist
@@ -116,9 +141,19 @@ def main():
     S = args.streams
     n_total = S * world
     s0, s1 = rt.fleet.shard_range(n_total, world, rank)
-    eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals)
-    eng.set_learning(False, False)
-    T = args.warmup + args.steps
+    if c3:
+        # fresh per-stream init (seeds 2045 + global stream index), learning on
+        cfg = rt.default_config(seg_capacity=args.seg_capacity, upd_capacity=512, seed_stride=1,
+                                sp_seed=2045 + s0, tm_seed=2045 + s0)
+        t0 = time.time()
+        eng = rt.HTMEngine(S, config=cfg, device=local)
+        torch.cuda.synchronize()
+        train_s, hdr = time.time() - t0, None
+        eng.set_learning(True, True)
+    else:
+        eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals)
+        eng.set_learning(False, False)
+    T = args.warmup + args.steps + args.lockstep_steps
     vals = torch.tensor(make_inputs(n_total, s0, s1, 0, T, trace), device=f"cuda:{local}")
     scores = torch.empty((T, S), dtype=torch.float32, device=f"cuda:{local}")
     gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
@@ -126,8 +161,8 @@ def main():
     if world > 1 and rank == 0:
         gathered = torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}")
 
-    for k in range(args.warmup):
-        eng.step(vals[k], out=scores[k])
+    if args.warmup:
+        eng.run(vals[:args.warmup], out=scores[:args.warmup])
     torch.cuda.synchronize()
     c0 = eng.counters()
     if not args.no_profile:
@@ -138,11 +173,14 @@ def main():
     t0 = time.perf_counter()
     handles = []
     if args.mode == "run":
-        eng.run(vals[args.warmup:], out=scores[args.warmup:])
-        if world > 1:
-            for k in range(args.steps):
-                h, _ = gather.gather(scores[args.warmup + k], staging=gathered[k] if rank == 0 else None)
-                handles.append(h)
+        for c0_ in range(0, args.steps, args.chunk):
+            m = min(args.chunk, args.steps - c0_)
+            a = args.warmup + c0_
+            eng.run(vals[a:a + m], out=scores[a:a + m])
+            if world > 1:  # the chunk's scores to rank 0 (SLO alerting), overlapped with the next chunk
+                for k in range(c0_, c0_ + m):
+                    h, _ = gather.gather(scores[args.warmup + k], staging=gathered[k] if rank == 0 else None)
+                    handles.append(h)
     else:
         for k in range(args.steps):
             eng.step(vals[args.warmup + k], out=scores[args.warmup + k])
@@ -166,16 +204,52 @@ def main():
         dt = float(t.item())
 
     value = n_total * args.steps / dt
+    lockstep = None
+    if args.lockstep_steps > 0:
+        # the same engine, lockstep: one htm_step per step (per-step kernel
+        # boundary = every stream waits for the slowest one each step)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        base = args.warmup + args.steps
+        for k in range(args.lockstep_steps):
+            eng.step(vals[base + k], out=scores[base + k])
+        torch.cuda.synchronize()
+        dl = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([dl], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dl = float(t.item())
+        lockstep = {"value": round(n_total * args.lockstep_steps / dl, 1), "steps": args.lockstep_steps,
+                    "ms_per_step": round(dl / args.lockstep_steps * 1e3, 4)}
     roof = None
+    sp_bytes = 0
+    if c3:
+        # SP learning per stream-step (not counted on the device): the 21 active
+        # input rows of the connected map, 40 active columns' potential
+        # permanences read+written, potential-mask rows, duty cycles read+written
+        # (SURVEY.md §8(d), weak-column bumps W excluded: a lower bound)
+        sp_bytes = 21 * 256 + 40 * 400 * 4 * 2 + 40 * 64 + 2 * 2048 * 4 * 2
     if prof is not None and prof["tm_ms"] > 0:
-        tm_bytes = c1["tm_bytes"] - c0["tm_bytes"]
+        tm_bytes = c1["tm_bytes"] - c0["tm_bytes"] + sp_bytes * S * args.steps
         launches = prof["launches"]
         avg_ms = prof["tm_ms"] / launches
         achieved = tm_bytes / launches / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = None, None
+        pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
+        if not c3 and os.path.exists(pmc):
+            # HBM bytes per stream-step of this kernel from the committed
+            # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py)
+            ps = json.load(open(pmc)).get("per_stream_step")
+            if ps:
+                traffic = int(ps["traffic"] * S * prof["steps"] / launches)
+                tsrc = "profiles/latest_pmc.json (FETCH_SIZE x2 + WRITE_SIZE per stream-step, x streams x steps/launch)"
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": ("htm_run_kernel<false,true> (fused SP+TM)" if prof["sp_ms"] == 0
-                           else "tm_step_kernel<false,true>"),
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
+                "kernel": (("htm_run_kernel<true,false> (fused SP+TM, learning)" if c3 else
+                            "htm_run_kernel<false,true> (fused SP+TM)") if eng.fused
+                           else "tm_step_kernel"),
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
                 "bytes_per_launch": int(tm_bytes / launches),
                 "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
@@ -183,17 +257,22 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "stream-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f32",
-        "data": "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config 2)",
-        "config": {"workload": "config2: Model-1 streams (2048-col SP, 12-cell BacktrackingTM), SP+TM learn off, "
-                               "from the GPU-trained Model-1 state",
+        "data": "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config %d)"
+                % args.config,
+        "config": {"workload": ("config3: fresh Model-1 streams (seed 2045+s), SP+TM learning on" if c3 else
+                                "config2: Model-1 streams (2048-col SP, 12-cell BacktrackingTM), SP+TM learn off, "
+                                "from the GPU-trained Model-1 state"),
                    "mode": args.mode,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": 2048, "cells_per_column": 12,
-                   "trained_segments": int(hdr.seg_live), "train_s": round(train_s, 2),
+                   "trained_segments": int(hdr.seg_live) if hdr is not None else None,
+                   "segments_after": int(c1["seg_live"] // S) if c3 else None,
+                   ("init_s" if c3 else "train_s"): round(train_s, 2),
                    "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL gather of scores" if world > 1 else "")},
         "roofline": roof,
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
+        "lockstep": lockstep,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not c3:
         out["cpu_baseline"] = cpu_baseline(trace, train_vals, n_total)
     if rank == 0:
         print(json.dumps(out), flush=True)

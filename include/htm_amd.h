@@ -243,6 +243,26 @@ size_t htm_device_bytes(const htm_engine* eng);
  * current. */
 int32_t htm_frozen_index_valid(const htm_engine* eng);
 
+/* ---- SLO-violation prediction harness, batched over streams ----------------
+ * ML/HTM/ModelTesting.py runModel :36-107, processpredictionList :113-146,
+ * getModelStats :148-171.  Per stream and record: the
+ * window of 1 + lookahead anomaly scores, the record's violation count and
+ * int(mean response time); a record with a missing metric is skipped
+ * (valid = 0).  Threshold 0.85 in the code, 0.98/0.99 in the README sweep;
+ * max_lead 50; slo_response 70 (ms). */
+typedef struct htm_slo htm_slo;
+int htm_slo_create(int32_t n_streams, double threshold, int32_t max_lead, int32_t slo_response, int32_t device,
+                   htm_slo** out);
+int htm_slo_destroy(htm_slo* slo);
+/* d_scores: DEVICE float [window][n_streams] (the engine's htm_run output
+ * rows of the record's steps); d_violations, d_means: DEVICE int32
+ * [n_streams]; d_valid: DEVICE uint8 [n_streams] or NULL (all valid). */
+int htm_slo_record(htm_slo* slo, const float* d_scores, int32_t window, const int32_t* d_violations,
+                   const int32_t* d_means, const uint8_t* d_valid, void* stream);
+/* getModelStats per stream into HOST h_out5[n_streams][5] = {TP, FP, TN, FN,
+ * lead-time sum} over the prediction list minus its last max_lead items. */
+int htm_slo_stats(htm_slo* slo, int64_t* h_out5, void* stream);
+
 const char* htm_last_error(void);
 int32_t htm_abi_version(void);
 

@@ -6,7 +6,8 @@ is not a Python identifier); it registers this package as `rtap_amd`.
 from . import _lib
 from ._lib import HtmConfig, HtmError, build, default_config
 from .engine import HTMEngine
-from . import fleet
+from . import fleet, harness
+from .harness import SLOHarness
 from .network import BatchRecordStream, MultiEncoder, Network, ScalarEncoder
 
-__all__ = ["HTMEngine", "Network", "BatchRecordStream", "MultiEncoder", "ScalarEncoder", "HtmConfig", "HtmError", "build", "default_config", "_lib"]
+__all__ = ["SLOHarness", "HTMEngine", "Network", "BatchRecordStream", "MultiEncoder", "ScalarEncoder", "HtmConfig", "HtmError", "build", "default_config", "_lib"]

@@ -94,6 +94,7 @@ EXPORTED = [
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
     "htm_profile_read", "htm_counters", "htm_debug_stamps",
+    "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats",
 ]
 
 _lib = None
@@ -159,6 +160,10 @@ def lib():
     L.htm_profile_read.argtypes = [vp, P(ctypes.c_double)]
     L.htm_counters.argtypes = [vp, P(ctypes.c_uint64)]
     L.htm_debug_stamps.argtypes = [vp, P(ctypes.c_uint64)]
+    L.htm_slo_create.argtypes = [i32, ctypes.c_double, i32, i32, i32, P(vp)]
+    L.htm_slo_destroy.argtypes = [vp]
+    L.htm_slo_record.argtypes = [vp, vp, i32, vp, vp, vp, vp]
+    L.htm_slo_stats.argtypes = [vp, P(ctypes.c_int64), vp]
     _lib = L
     return L
 

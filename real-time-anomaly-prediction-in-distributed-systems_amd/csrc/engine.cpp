@@ -201,8 +201,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.n_streams = n;
     d.max_act_cells = d.num_desired * d.K;
     d.q_lds = 1024;
-    d.fin_sorted = 1;
-    if (const char* env = std::getenv("HTM_TM_FIN")) d.fin_sorted = std::strcmp(env, "buckets") != 0;
+    d.fin_sorted = 0;  // measured: column buckets beat the bitonic key sort at Model-1 sizes
+    if (const char* env = std::getenv("HTM_TM_FIN")) d.fin_sorted = std::strcmp(env, "sorted") == 0;
     // frozen-inference counter window: the union region holds the u8
     // counters (fx_win bytes) plus the active-cell list and its block prefix;
     // fill the LDS budget (two workgroups per CU by default).  Out-list
@@ -270,13 +270,8 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.scr_conf, float, S * d.ncol);
     ALLOC(e->tm.scr_q, uint32_t, S * cap);
     ALLOC(e->tm.scr_q2, uint32_t, S * cap);
-    ALLOC(e->tm.scr_cur, uint32_t, S * (size_t)d.fx_noff);
     ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
     ALLOC(e->tm.fx_base, uint64_t, S);
-    ALLOC(e->tm.fx_off, uint32_t, S * (size_t)d.fx_noff);
-    ALLOC(e->tm.fx_rec, uint2, S * cap);
-    ALLOC(e->tm.fx_pcell, uint16_t, S * (size_t)d.fx_pcap);
-    ALLOC(e->tm.fx_np, uint32_t, S);
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
     ALLOC(e->tm.dbg, uint64_t, S * 32);
@@ -419,8 +414,24 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
 
 }  // extern "C"
 
+// The frozen index's per-stream tables are allocated on first use, so an
+// engine that only learns (config 3) does not pay for them.
+static int alloc_fx(htm_engine* e) {
+    if (e->tm.fx_off) return HTM_OK;
+    const DevCfg& d = e->dc;
+    const size_t S = (size_t)e->n;
+    ALLOC(e->tm.scr_cur, uint32_t, S * (size_t)d.fx_noff);
+    ALLOC(e->tm.fx_off, uint32_t, S * (size_t)d.fx_noff);
+    ALLOC(e->tm.fx_rec, uint2, S * (size_t)d.seg_cap);
+    ALLOC(e->tm.fx_pcell, uint16_t, S * (size_t)d.fx_pcap);
+    ALLOC(e->tm.fx_np, uint32_t, S);
+    return HTM_OK;
+}
+
 static int build_fx(htm_engine* e, hipStream_t st) {
     const DevCfg& d = e->dc;
+    int ra = alloc_fx(e);
+    if (ra) return ra;
     if (launch_tm_fx_count(d, e->tm, e->d_counts, e->n, st)) return fail(HTM_E_HIP, "fx count launch");
     std::vector<uint64_t> counts((size_t)e->n);
     HIP_TRY(hipMemcpyAsync(counts.data(), e->d_counts, counts.size() * 8, hipMemcpyDeviceToHost, st));

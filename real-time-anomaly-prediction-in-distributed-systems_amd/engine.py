@@ -11,6 +11,7 @@ ModelTesting.py; this engine replaces that per-stream loop.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -48,6 +49,7 @@ class HTMEngine:
         self.n_cells = cfg.sp_columns * cfg.tm_cells_per_col
         self.sp_learn = True
         self.tm_learn = True
+        self.fused = os.environ.get("HTM_FUSED", "1") != "0"  # the engine's default (HTM_OPT_FUSED)
 
     # ------------------------------------------------------------------ life
     def close(self):
@@ -176,6 +178,7 @@ class HTMEngine:
     def use_fused(self, on: bool):
         """One fused SP+TM kernel per step / per htm_run chunk (default on)."""
         self.set_option(_lib.OPT_FUSED, int(on))
+        self.fused = bool(on)
 
     def set_run_chunk(self, steps: int):
         """Steps per fused htm_run launch."""
