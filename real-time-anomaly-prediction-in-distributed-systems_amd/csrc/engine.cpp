@@ -200,7 +200,18 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     if (d.seg_reserve >= d.seg_cap) return fail(HTM_E_INVALID, "seg_capacity too small for one learning step");
     d.n_streams = n;
     d.max_act_cells = d.num_desired * d.K;
-    d.q_lds = 1024;
+    // qualifying segments ranked in LDS: as many (<= 1024) as the phase-2
+    // bucket arrays leave room for in the LDS budget; more go through HBM
+    {
+        const size_t off_u0 = tm_step_lds_base(d, 0, 1);
+        const size_t avail0 = lds_budget > off_u0 ? (lds_budget - off_u0) / 4 : 0;
+        const size_t fixed = (size_t)d.ncol + (size_t)(d.ncol + 1) / 2 + (size_t)d.ncol + 1;
+        size_t q = avail0 > fixed ? (avail0 - fixed) * 2 / 9 : 0;
+        q = q / 64 * 64;
+        if (q > 1024) q = 1024;
+        if (q < 64) return fail(HTM_E_INVALID, "LDS budget %zu too small for the phase-2 buckets", lds_budget);
+        d.q_lds = (int32_t)q;
+    }
     d.fin_sorted = 0;  // measured: column buckets beat the bitonic key sort at Model-1 sizes
     if (const char* env = std::getenv("HTM_TM_FIN")) d.fin_sorted = std::strcmp(env, "sorted") == 0;
     // frozen-inference counter window: the union region holds the u8
@@ -208,7 +219,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // fill the LDS budget (two workgroups per CU by default).  Out-list
     // entries are window-relative u16 with 0xFFFF as padding.
     const size_t off_u = tm_step_lds_base(d, 0, 1);
-    const size_t cell_words = (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1;
+    const size_t cell_words = (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1 + FX_OWN / 2;
     size_t avail = lds_budget > off_u ? (lds_budget - off_u) / 4 : 0;
     size_t win = avail > cell_words ? (avail - cell_words) * 4 : 0;
     win = (win / 1024) * 1024;

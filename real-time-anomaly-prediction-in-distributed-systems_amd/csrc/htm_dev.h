@@ -18,6 +18,11 @@
 #define HTM_MAXPAT 16     // backtrack pattern history slots
 #define HTM_NPLANES 7     // bit-sliced overlap planes (overlap <= 127)
 #define HTM_MAXNW 128     // ncol/32 words (ncol <= 4096)
+#define TM_NT 256                  // threads of the TM workgroup (one stream)
+#define TM_NWAVES (TM_NT / 64)
+#define FX_DEPTH 8                 // frozen index: out-list blocks in flight per thread
+#define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
+#define FX_MAXPER 8                // active cells per thread (<= 64 columns x 32 cells / TM_NT)
 
 // Derived, immutable engine constants (kernel argument).
 struct DevCfg {

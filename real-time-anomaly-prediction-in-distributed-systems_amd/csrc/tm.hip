@@ -28,11 +28,7 @@
 //     wave 0 in NuPIC order; everything else is wave- or workgroup-parallel.
 #include "sp_dev.h"
 
-#define TM_NT 256
-#define TM_NWAVES (TM_NT / 64)
-#define FX_DEPTH 8                 // out-list blocks in flight per thread
-#define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
-#define FX_MAXPER 8                // active cells per thread (<= 64 columns x 32 cells / TM_NT)
+
 
 __constant__ float kDcAlpha[9] = {0.0f, 0.0032f, 0.0010f, 0.00032f, 0.00010f, 0.000032f, 0.00001f, 0.0000032f, 0.0000010f};
 __constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 100000, 320000};
@@ -280,35 +276,68 @@ __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA
 
 // collect slots of segments with >= thr synapses onto active cells of
 // `state` by scanning the pool (learning-on form)
-__device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
+// Scan the segment pool (4 lanes per segment, 16 B of synapse sources each)
+// against the cell bitmap `state`: for every slot, f(slot, meta, eligible,
+// mask of synapses onto cells on in `state`) on all 4 lanes (mask reduced
+// across them).  Only segments with elig(meta) load their rows.  SC_DEPTH
+// batches of 64 segments are in flight per workgroup: meta loads of the
+// batch first, then the row loads, so a pass over the pool costs two HBM
+// round trips per SC_DEPTH x 64 segments.  Returns this thread's bytes.
+#define SC_DEPTH 8
+template <typename E, typename F>
+__device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E elig, F f) {
     const uint32_t hwm = t.sh->hwm;
-    const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
-    uint32_t nb = 0;  // bytes read by this thread
-    for (uint32_t base = 0; base < hwm; base += TM_NT / 4) {
-        uint32_t slot = base + g;
-        uint32_t m = slot < hwm ? t.meta[slot] : 0u;
-        if (slot < hwm && sub == 0) nb += 4;
-        uint32_t nsyn = meta_nsyn(m);
-        bool live = meta_live(m);
-        uint32_t mask = 0;
-        if (live && (uint32_t)(sub * 8) < nsyn) {
-            nb += 16;
-            uint4 v = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
-            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    uint32_t nb = 0;
+    for (uint32_t base = 0; base < hwm; base += SC_DEPTH * (TM_NT / 4)) {
+        uint32_t m[SC_DEPTH];
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                uint32_t j = sub * 8 + k;
-                uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-                if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
-            }
+        for (int d = 0; d < SC_DEPTH; d++) {
+            const uint32_t slot = base + d * (TM_NT / 4) + g;
+            m[d] = slot < hwm ? t.meta[slot] : 0u;
         }
-        mask |= __shfl_xor(mask, 1, 64);
-        mask |= __shfl_xor(mask, 2, 64);
-        if (live && sub == 0 && __popc(mask) >= thr) {
-            int i = atomicAdd(&t.sh->qn, 1);
-            t.q1[i] = slot;
+        uint4 v[SC_DEPTH];
+        bool el[SC_DEPTH];
+#pragma unroll
+        for (int d = 0; d < SC_DEPTH; d++) {
+            const uint32_t slot = base + d * (TM_NT / 4) + g;
+            el[d] = meta_live(m[d]) && elig(m[d]);
+            v[d] = make_uint4(0u, 0u, 0u, 0u);
+            if (el[d] && sub * 8u < meta_nsyn(m[d]))
+                v[d] = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
+        }
+#pragma unroll
+        for (int d = 0; d < SC_DEPTH; d++) {
+            const uint32_t slot = base + d * (TM_NT / 4) + g;
+            if (slot < hwm && sub == 0) nb += 4;
+            const uint32_t nsyn = meta_nsyn(m[d]);
+            uint32_t mask = 0;
+            if (el[d] && sub * 8u < nsyn) {
+                nb += 16;
+                const uint32_t w[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t j = sub * 8 + k;
+                    const uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+                    if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
+                }
+            }
+            mask |= __shfl_xor(mask, 1, 64);
+            mask |= __shfl_xor(mask, 2, 64);
+            f(slot, m[d], el[d], mask);
         }
     }
+    return nb;
+}
+
+// collect slots of segments with >= thr synapses onto active cells of
+// `state` by scanning the pool (learning-on form)
+__device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
+    const uint32_t sub = threadIdx.x & 3;
+    uint32_t nb = scan_pool(t, state, [](uint32_t) { return true; },
+                            [&](uint32_t slot, uint32_t, bool el, uint32_t mask) {
+                                if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) t.q1[atomicAdd(&t.sh->qn, 1)] = slot;
+                            });
     nb = wg_sum(t.sh, nb);
     if (threadIdx.x == 0) t.sh->bytes += nb;
     STAMP(t, SB_SCAN);
@@ -947,38 +976,23 @@ __device__ __forceinline__ void update_inference(Tm& t) {
 __device__ __forceinline__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t* colflags) {
     const DevCfg& c = t.c;
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
-    const uint32_t hwm = t.sh->hwm;
-    const int g = threadIdx.x >> 2, sub = threadIdx.x & 3;
-    uint32_t nb = 0;
-    for (uint32_t base = 0; base < hwm; base += TM_NT / 4) {
-        uint32_t slot = base + g;
-        uint32_t m = slot < hwm ? t.meta[slot] : 0u;
-        if (slot < hwm && sub == 0) nb += 4;
-        uint32_t nsyn = meta_nsyn(m), cell = meta_cell(m);
-        uint32_t col = col_of(c, cell);
-        bool elig = meta_live(m) && (!colflags || ((colflags[col >> 5] >> (col & 31)) & 1u));
-        uint32_t mask = 0;
-        if (elig && (uint32_t)(sub * 8) < nsyn) {
-            nb += 16;
-            uint4 v = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
-            uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                uint32_t j = sub * 8 + k;
-                uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-                if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
+    const uint32_t sub = threadIdx.x & 3;
+    uint32_t nb = scan_pool(
+        t, state,
+        [&](uint32_t m) {
+            const uint32_t col = col_of(c, meta_cell(m));
+            return !colflags || ((colflags[col >> 5] >> (col & 31)) & 1u);
+        },
+        [&](uint32_t slot, uint32_t m, bool el, uint32_t mask) {
+            const uint32_t n = __popc(mask);
+            if (el && sub == 0 && n >= (uint32_t)thr) {
+                const uint32_t cell = meta_cell(m), col = col_of(c, cell);
+                const uint32_t cic = cell - col * c.K;
+                const unsigned long long key = ((unsigned long long)n << 40) | ((unsigned long long)cic << 32) |
+                                               (unsigned long long)(0xFFFFFFFFu - slot);
+                atomicMax(&keys[col], key);
             }
-        }
-        mask |= __shfl_xor(mask, 1, 64);
-        mask |= __shfl_xor(mask, 2, 64);
-        uint32_t n = __popc(mask);
-        if (elig && sub == 0 && n >= (uint32_t)thr) {
-            uint32_t cic = cell - col * c.K;
-            unsigned long long key = ((unsigned long long)n << 40) | ((unsigned long long)cic << 32) |
-                                     (unsigned long long)(0xFFFFFFFFu - slot);
-            atomicMax(&keys[col], key);
-        }
-    }
+        });
     nb = wg_sum(t.sh, nb);
     if (threadIdx.x == 0) t.sh->bytes += nb;
 }
@@ -1563,6 +1577,10 @@ __device__ __forceinline__ void compact_pool(Tm& t) {
         uint32_t mm = 0, cm = 0, d0 = 0, d1 = 0, d2 = 0;
         uint4 sv[4];
         float4 pv[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) sv[k] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < 8; k++) pv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ns != 0xFFFFFFFFu) {
             mm = t.meta[slot];
             cm = t.conn[slot];
