@@ -91,9 +91,10 @@ def cpu_baseline(trace, train_vals, n_total, target_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", type=int, choices=[2, 3], default=2,
+    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=2,
                     help="2 (default, the metric's config): trained Model-1 streams, learning off; "
-                         "3: fresh streams (seed 2045 + s), SP+TM learning on, 256 steps")
+                         "3: fresh streams (seed 2045 + s), SP+TM learning on, 256 steps; "
+                         "4: fleet -- 131,072 streams per GPU sharing one frozen trained model")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: 2324, config 3: 240)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config 2: 64, config 3: 16)")
     ap.add_argument("--streams", type=int, default=None,
@@ -110,17 +111,20 @@ def main():
     ap.add_argument("--lockstep-steps", type=int, default=256,
                     help="after the timed region, also time this many lockstep htm_step steps (0: skip)")
     args = ap.parse_args()
-    c3 = args.config == 3
+    c3, c4 = args.config == 3, args.config == 4
     if args.steps is None:
-        args.steps = 240 if c3 else 2324
+        args.steps = 240 if c3 else 256 if c4 else 2324
     if args.warmup is None:
-        args.warmup = 16 if c3 else 64
+        args.warmup = 16 if (c3 or c4) else 64
     if args.streams is None:
-        args.streams = 40960 if c3 else 1024
+        args.streams = 40960 if c3 else 131072 if c4 else 1024
     if args.seg_capacity is None:
         args.seg_capacity = 10240 if c3 else 72 * 1024
     if c3:
         args.lockstep_steps = 0
+    if c4:
+        args.chunk = min(args.chunk, 64)
+        args.lockstep_steps = min(args.lockstep_steps, 32)
 
     import torch
     import torch.distributed as dist
@@ -150,11 +154,24 @@ def main():
         torch.cuda.synchronize()
         train_s, hdr = time.time() - t0, None
         eng.set_learning(True, True)
+    elif c4:
+        # one model trained on the GPU (2184 Model-1 records), shared by every stream
+        model, train_s, hdr = trained_engine(rt, 1, args.seg_capacity, local, train_vals)
+        eng = rt.HTMEngine.fleet(model, S, q_capacity=4096)
+        model.close()
     else:
         eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals)
         eng.set_learning(False, False)
     T = args.warmup + args.steps + args.lockstep_steps
-    vals = torch.tensor(make_inputs(n_total, s0, s1, 0, T, trace), device=f"cuda:{local}")
+    if c4:
+        # per-rank jitter stream (a 1M x T matrix per rank would not fit host memory)
+        rng = np.random.Generator(np.random.PCG64([724, s0]))
+        t_ = np.arange(T)[:, None]
+        g_ = np.arange(s0, s1)[None, :]
+        vals = torch.tensor(np.clip(trace[(t_ + 97 * g_) % len(trace)] + rng.integers(-2, 3, size=(T, S)), 0, 100)
+                            .astype(np.float64), device=f"cuda:{local}")
+    else:
+        vals = torch.tensor(make_inputs(n_total, s0, s1, 0, T, trace), device=f"cuda:{local}")
     scores = torch.empty((T, S), dtype=torch.float32, device=f"cuda:{local}")
     gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
     gathered = None
@@ -238,7 +255,7 @@ def main():
         achieved = tm_bytes / launches / (avg_ms * 1e-3) / 1e9
         traffic, tsrc = None, None
         pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
-        if not c3 and os.path.exists(pmc):
+        if not c3 and not c4 and os.path.exists(pmc):
             # HBM bytes per stream-step of this kernel from the committed
             # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py)
             ps = json.load(open(pmc)).get("per_stream_step")
@@ -248,6 +265,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": (("htm_run_kernel<true,false> (fused SP+TM, learning)" if c3 else
+                            "htm_run_kernel<false,true> (fused SP+TM, fleet: shared model)" if c4 else
                             "htm_run_kernel<false,true> (fused SP+TM)") if eng.fused
                            else "tm_step_kernel"),
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
@@ -260,6 +278,8 @@ def main():
         "data": "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config %d)"
                 % args.config,
         "config": {"workload": ("config3: fresh Model-1 streams (seed 2045+s), SP+TM learning on" if c3 else
+                                "config4 fleet: streams sharing one frozen GPU-trained Model-1 SP+TM, "
+                                "per-stream TM state, learn off" if c4 else
                                 "config2: Model-1 streams (2048-col SP, 12-cell BacktrackingTM), SP+TM learn off, "
                                 "from the GPU-trained Model-1 state"),
                    "mode": args.mode,
@@ -272,7 +292,7 @@ def main():
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
         "lockstep": lockstep,
     }
-    if rank == 0 and world == 1 and not args.no_cpu and not c3:
+    if rank == 0 and world == 1 and not args.no_cpu and not c3 and not c4:
         out["cpu_baseline"] = cpu_baseline(trace, train_vals, n_total)
     if rank == 0:
         print(json.dumps(out), flush=True)

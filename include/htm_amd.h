@@ -234,6 +234,20 @@ int htm_load(const char* path, int32_t device, htm_engine** out);
  * every stream starts from the same trained Model-1 state). */
 int htm_replicate_stream(htm_engine* eng, int32_t src, void* stream);
 
+/* Fleet mode: n_streams streams that share ONE
+ * frozen model -- the SP and the TM segment pool of stream `model_stream` of
+ * `model` -- each with its own TM state (cell bitmaps, confidences, pattern
+ * history, counters), every stream starting from the model stream's state.
+ * Learning stays off (htm_set_learning with a flag on: HTM_E_STATE); with
+ * learning off replicated models never diverge, so a fleet's results equal
+ * those of an ordinary engine holding n_streams copies of the model, at a
+ * fraction of the memory.  q_capacity bounds each stream's list of
+ * qualifying segments per inference pass (overflow: htm_status reports
+ * error flag 16). */
+int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_streams, int32_t q_capacity,
+                     int32_t device, htm_engine** out);
+int32_t htm_is_fleet(const htm_engine* eng);
+
 /* Engine introspection */
 int32_t htm_n_streams(const htm_engine* eng);
 int htm_get_config(const htm_engine* eng, htm_config* out);
@@ -262,6 +276,21 @@ int htm_slo_record(htm_slo* slo, const float* d_scores, int32_t window, const in
 /* getModelStats per stream into HOST h_out5[n_streams][5] = {TP, FP, TN, FN,
  * lead-time sum} over the prediction list minus its last max_lead items. */
 int htm_slo_stats(htm_slo* slo, int64_t* h_out5, void* stream);
+
+/* ---- AnomalyLikelihood, batched over streams (north-star extension; the
+ * reference never computes it, parity unpinned) ------------------------------
+ * NuPIC 1.0.x AnomalyLikelihood semantics (oracle/likelihood_reference.py):
+ * learning_period 288, estimation_samples 100, historic_window 8640 (<= 8640),
+ * reestimation_period 100 are NuPIC's defaults. */
+typedef struct htm_likelihood htm_likelihood;
+int htm_likelihood_create(int32_t n_streams, int32_t learning_period, int32_t estimation_samples,
+                          int32_t historic_window, int32_t reestimation_period, int32_t device, htm_likelihood** out);
+int htm_likelihood_destroy(htm_likelihood* lk);
+/* anomalyProbability(value, anomalyScore) of every stream: d_values DEVICE
+ * double, stream s's metric at d_values[s * value_stride]; d_scores DEVICE
+ * float [n] (the engine's raw scores); d_out DEVICE double [n]. */
+int htm_likelihood_step(htm_likelihood* lk, const double* d_values, int32_t value_stride, const float* d_scores,
+                        double* d_out, void* stream);
 
 const char* htm_last_error(void);
 int32_t htm_abi_version(void);

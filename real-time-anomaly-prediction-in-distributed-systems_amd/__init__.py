@@ -7,7 +7,7 @@ from . import _lib
 from ._lib import HtmConfig, HtmError, build, default_config
 from .engine import HTMEngine
 from . import fleet, harness
-from .harness import SLOHarness
+from .harness import AnomalyLikelihood, SLOHarness
 from .network import BatchRecordStream, MultiEncoder, Network, ScalarEncoder
 
-__all__ = ["SLOHarness", "HTMEngine", "Network", "BatchRecordStream", "MultiEncoder", "ScalarEncoder", "HtmConfig", "HtmError", "build", "default_config", "_lib"]
+__all__ = ["AnomalyLikelihood", "SLOHarness", "HTMEngine", "Network", "BatchRecordStream", "MultiEncoder", "ScalarEncoder", "HtmConfig", "HtmError", "build", "default_config", "_lib"]

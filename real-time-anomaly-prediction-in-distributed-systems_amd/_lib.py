@@ -14,6 +14,9 @@ LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd.so")
 # diagnostic build with per-phase cycle stamps (tools/ only): HTM_AMD_STAMPS=1
 if os.environ.get("HTM_AMD_STAMPS") == "1":
     LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd_stamps.so")
+# experiment builds (make variant ...; tools/ only)
+if os.environ.get("HTM_AMD_LIB"):
+    LIB_PATH = os.path.join(PKG_DIR, os.environ["HTM_AMD_LIB"])
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 HTM_OK = 0
@@ -94,7 +97,8 @@ EXPORTED = [
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
     "htm_profile_read", "htm_counters", "htm_debug_stamps",
-    "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats",
+    "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats", "htm_create_fleet", "htm_is_fleet",
+    "htm_likelihood_create", "htm_likelihood_destroy", "htm_likelihood_step",
 ]
 
 _lib = None
@@ -160,6 +164,12 @@ def lib():
     L.htm_profile_read.argtypes = [vp, P(ctypes.c_double)]
     L.htm_counters.argtypes = [vp, P(ctypes.c_uint64)]
     L.htm_debug_stamps.argtypes = [vp, P(ctypes.c_uint64)]
+    L.htm_create_fleet.argtypes = [vp, i32, i32, i32, i32, P(vp)]
+    L.htm_is_fleet.argtypes = [vp]
+    L.htm_is_fleet.restype = i32
+    L.htm_likelihood_create.argtypes = [i32, i32, i32, i32, i32, i32, P(vp)]
+    L.htm_likelihood_destroy.argtypes = [vp]
+    L.htm_likelihood_step.argtypes = [vp, vp, i32, vp, vp, vp]
     L.htm_slo_create.argtypes = [i32, ctypes.c_double, i32, i32, i32, P(vp)]
     L.htm_slo_destroy.argtypes = [vp]
     L.htm_slo_record.argtypes = [vp, vp, i32, vp, vp, vp, vp]

@@ -8,6 +8,7 @@
 // step after learning, one count/scan/fill pass per stream).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -45,12 +46,15 @@ size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct Region {
     void* base;
     size_t per_stream;
+    bool model;  // part of the model (SP permanences/connections, TM segment pool): one instance in a fleet
 };
 
 struct htm_engine {
     htm_config cfg;
     DevCfg dc;
     int32_t n;
+    int32_t nm = 0;      // model instances: n, or 1 in a fleet (shared model)
+    bool fleet = false;
     int32_t device;
     SpBufs sp;
     TmBufs tm;
@@ -199,6 +203,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.seg_reserve = (c.tm_max_lrn_backtrack + 2) * c.sp_num_active;
     if (d.seg_reserve >= d.seg_cap) return fail(HTM_E_INVALID, "seg_capacity too small for one learning step");
     d.n_streams = n;
+    d.shared_model = 0;
+    d.q_cap = d.seg_cap;
     d.max_act_cells = d.num_desired * d.K;
     // qualifying segments ranked in LDS: as many (<= 1024) as the phase-2
     // bucket arrays leave room for in the LDS budget; more go through HBM
@@ -256,11 +262,12 @@ static int dalloc(htm_engine* e, void** p, size_t bytes) {
 static int allocate(htm_engine* e) {
     const DevCfg& d = e->dc;
     const size_t S = (size_t)e->n;
+    const size_t M = (size_t)e->nm;  // model instances
     const size_t cap = (size_t)d.seg_cap;
-    ALLOC(e->sp.connT, uint32_t, S * d.nin_pad * d.nw);
-    ALLOC(e->sp.potmask, uint32_t, S * d.ncol * (d.nin_pad / 32));
-    ALLOC(e->sp.perm, float, S * d.ncol * d.n_potential);
-    ALLOC(e->sp.duty, float, S * 2 * d.ncol);
+    ALLOC(e->sp.connT, uint32_t, M * d.nin_pad * d.nw);
+    ALLOC(e->sp.potmask, uint32_t, M * d.ncol * (d.nin_pad / 32));
+    ALLOC(e->sp.perm, float, M * d.ncol * d.n_potential);
+    ALLOC(e->sp.duty, float, M * 2 * d.ncol);
     ALLOC(e->sp.scalars, uint32_t, S * 4);
     ALLOC(e->sp.act, uint16_t, S * HTM_MAXACT);
     ALLOC(e->sp.nact, uint32_t, S);
@@ -270,17 +277,17 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.bm, uint32_t, S * 4 * d.cw);
     ALLOC(e->tm.colconf, float, S * d.ncol);
     ALLOC(e->tm.pat, uint16_t, S * 2 * HTM_MAXPAT * HTM_MAXACT);
-    ALLOC(e->tm.seg_meta, uint32_t, S * cap);
-    ALLOC(e->tm.seg_src, uint16_t, S * cap * HTM_MAXSYN);
-    ALLOC(e->tm.seg_perm, float, S * cap * HTM_MAXSYN);
-    ALLOC(e->tm.seg_conn, uint32_t, S * cap);
-    ALLOC(e->tm.seg_duty, uint32_t, S * cap * 3);
-    ALLOC(e->tm.cell_nseg, uint8_t, S * d.ncells);
-    ALLOC(e->tm.upd, htm_tm_update, S * d.upd_cap);
+    ALLOC(e->tm.seg_meta, uint32_t, M * cap);
+    ALLOC(e->tm.seg_src, uint16_t, M * cap * HTM_MAXSYN);
+    ALLOC(e->tm.seg_perm, float, M * cap * HTM_MAXSYN);
+    ALLOC(e->tm.seg_conn, uint32_t, M * cap);
+    ALLOC(e->tm.seg_duty, uint32_t, M * cap * 3);
+    ALLOC(e->tm.cell_nseg, uint8_t, M * d.ncells);
+    ALLOC(e->tm.upd, htm_tm_update, M * d.upd_cap);
     ALLOC(e->tm.scr_bm, uint32_t, S * 5 * d.cw);
     ALLOC(e->tm.scr_conf, float, S * d.ncol);
-    ALLOC(e->tm.scr_q, uint32_t, S * cap);
-    ALLOC(e->tm.scr_q2, uint32_t, S * cap);
+    ALLOC(e->tm.scr_q, uint32_t, S * (size_t)d.q_cap);
+    ALLOC(e->tm.scr_q2, uint32_t, std::max(S * (size_t)d.q_cap, cap));
     ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
@@ -290,23 +297,23 @@ static int allocate(htm_engine* e) {
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
     Region* r = e->regions;
-    for (int i = 0; i < 17; i++) r[i] = Region{nullptr, 0};
-    r[HTM_ST_SP_CONNT] = {e->sp.connT, (size_t)d.nin_pad * d.nw * 4};
-    r[HTM_ST_SP_POTMASK] = {e->sp.potmask, (size_t)d.ncol * (d.nin_pad / 32) * 4};
-    r[HTM_ST_SP_PERM] = {e->sp.perm, (size_t)d.ncol * d.n_potential * 4};
-    r[HTM_ST_SP_DUTY] = {e->sp.duty, (size_t)2 * d.ncol * 4};
-    r[HTM_ST_SP_SCALARS] = {e->sp.scalars, 16};
-    r[HTM_ST_TM_HEADER] = {e->tm.hdr, sizeof(htm_tm_header)};
-    r[HTM_ST_TM_BITMAPS] = {e->tm.bm, (size_t)4 * d.cw * 4};
-    r[HTM_ST_TM_COLCONF] = {e->tm.colconf, (size_t)d.ncol * 4};
-    r[HTM_ST_TM_SEG_META] = {e->tm.seg_meta, cap * 4};
-    r[HTM_ST_TM_SEG_SRC] = {e->tm.seg_src, cap * HTM_MAXSYN * 2};
-    r[HTM_ST_TM_SEG_PERM] = {e->tm.seg_perm, cap * HTM_MAXSYN * 4};
-    r[HTM_ST_TM_SEG_CONN] = {e->tm.seg_conn, cap * 4};
-    r[HTM_ST_TM_SEG_DUTY] = {e->tm.seg_duty, cap * 12};
-    r[HTM_ST_TM_CELL_NSEG] = {e->tm.cell_nseg, (size_t)d.ncells};
-    r[HTM_ST_TM_PATTERNS] = {e->tm.pat, (size_t)2 * HTM_MAXPAT * HTM_MAXACT * 2};
-    r[HTM_ST_TM_UPDATES] = {e->tm.upd, (size_t)d.upd_cap * sizeof(htm_tm_update)};
+    for (int i = 0; i < 17; i++) r[i] = Region{nullptr, 0, false};
+    r[HTM_ST_SP_CONNT] = {e->sp.connT, (size_t)d.nin_pad * d.nw * 4, true};
+    r[HTM_ST_SP_POTMASK] = {e->sp.potmask, (size_t)d.ncol * (d.nin_pad / 32) * 4, true};
+    r[HTM_ST_SP_PERM] = {e->sp.perm, (size_t)d.ncol * d.n_potential * 4, true};
+    r[HTM_ST_SP_DUTY] = {e->sp.duty, (size_t)2 * d.ncol * 4, true};
+    r[HTM_ST_SP_SCALARS] = {e->sp.scalars, 16, false};
+    r[HTM_ST_TM_HEADER] = {e->tm.hdr, sizeof(htm_tm_header), false};
+    r[HTM_ST_TM_BITMAPS] = {e->tm.bm, (size_t)4 * d.cw * 4, false};
+    r[HTM_ST_TM_COLCONF] = {e->tm.colconf, (size_t)d.ncol * 4, false};
+    r[HTM_ST_TM_SEG_META] = {e->tm.seg_meta, cap * 4, true};
+    r[HTM_ST_TM_SEG_SRC] = {e->tm.seg_src, cap * HTM_MAXSYN * 2, true};
+    r[HTM_ST_TM_SEG_PERM] = {e->tm.seg_perm, cap * HTM_MAXSYN * 4, true};
+    r[HTM_ST_TM_SEG_CONN] = {e->tm.seg_conn, cap * 4, true};
+    r[HTM_ST_TM_SEG_DUTY] = {e->tm.seg_duty, cap * 12, true};
+    r[HTM_ST_TM_CELL_NSEG] = {e->tm.cell_nseg, (size_t)d.ncells, true};
+    r[HTM_ST_TM_PATTERNS] = {e->tm.pat, (size_t)2 * HTM_MAXPAT * HTM_MAXACT * 2, false};
+    r[HTM_ST_TM_UPDATES] = {e->tm.upd, (size_t)d.upd_cap * sizeof(htm_tm_update), true};
     return HTM_OK;
 }
 
@@ -332,13 +339,16 @@ static int check_lds(const DevCfg& d) {
     return HTM_OK;
 }
 
-static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out) {
+static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out,
+                         int32_t fleet_q_cap = 0) {
     if (!cfg || !out || n_streams < 1) return fail(HTM_E_INVALID, "bad arguments");
     *out = nullptr;
     HIP_TRY(hipSetDevice(device));
     htm_engine* e = new htm_engine();
     e->cfg = *cfg;
     e->n = n_streams;
+    e->fleet = fleet_q_cap > 0;
+    e->nm = e->fleet ? 1 : n_streams;
     e->device = device;
     int optin = query_lds_optin();
     size_t budget = optin >= 78 * 1024 ? (size_t)76 * 1024 : (size_t)optin - 2048;
@@ -348,6 +358,11 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     }
     if (const char* env = std::getenv("HTM_FUSED")) e->fused = std::atoi(env) != 0;  // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
+    if (!r && e->fleet) {
+        e->dc.shared_model = 1;
+        e->dc.q_cap = std::min(fleet_q_cap, e->dc.seg_cap);
+        e->sp_learn = e->tm_learn = 0;
+    }
     if (!r) r = check_lds(e->dc);
     if (!r) r = allocate(e);
     if (!r && tm_configure_lds(e->dc)) {
@@ -398,6 +413,8 @@ int htm_destroy(htm_engine* e) {
 
 int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
     if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (e->fleet && (sp_learn || tm_learn))
+        return fail(HTM_E_STATE, "a fleet engine shares one frozen model: learning stays off");
     e->sp_learn = sp_learn ? 1 : 0;
     if (tm_learn && !e->tm_learn) e->fx_valid = false;
     e->tm_learn = tm_learn ? 1 : 0;
@@ -430,12 +447,12 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
 static int alloc_fx(htm_engine* e) {
     if (e->tm.fx_off) return HTM_OK;
     const DevCfg& d = e->dc;
-    const size_t S = (size_t)e->n;
-    ALLOC(e->tm.scr_cur, uint32_t, S * (size_t)d.fx_noff);
-    ALLOC(e->tm.fx_off, uint32_t, S * (size_t)d.fx_noff);
-    ALLOC(e->tm.fx_rec, uint2, S * (size_t)d.seg_cap);
-    ALLOC(e->tm.fx_pcell, uint16_t, S * (size_t)d.fx_pcap);
-    ALLOC(e->tm.fx_np, uint32_t, S);
+    const size_t M = (size_t)e->nm;
+    ALLOC(e->tm.scr_cur, uint32_t, M * (size_t)d.fx_noff);
+    ALLOC(e->tm.fx_off, uint32_t, M * (size_t)d.fx_noff);
+    ALLOC(e->tm.fx_rec, uint2, M * (size_t)d.seg_cap);
+    ALLOC(e->tm.fx_pcell, uint16_t, M * (size_t)d.fx_pcap);
+    ALLOC(e->tm.fx_np, uint32_t, M);
     return HTM_OK;
 }
 
@@ -443,13 +460,13 @@ static int build_fx(htm_engine* e, hipStream_t st) {
     const DevCfg& d = e->dc;
     int ra = alloc_fx(e);
     if (ra) return ra;
-    if (launch_tm_fx_count(d, e->tm, e->d_counts, e->n, st)) return fail(HTM_E_HIP, "fx count launch");
-    std::vector<uint64_t> counts((size_t)e->n);
+    if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return fail(HTM_E_HIP, "fx count launch");
+    std::vector<uint64_t> counts((size_t)e->nm);
     HIP_TRY(hipMemcpyAsync(counts.data(), e->d_counts, counts.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    std::vector<uint64_t> base((size_t)e->n);
+    std::vector<uint64_t> base((size_t)e->nm);
     uint64_t tot = 0;
-    for (int s = 0; s < e->n; s++) {
+    for (int s = 0; s < e->nm; s++) {
         base[s] = tot;
         tot += counts[s];
     }
@@ -463,7 +480,7 @@ static int build_fx(htm_engine* e, hipStream_t st) {
     }
     HIP_TRY(hipMemsetAsync(e->tm.fx_ent, 0xFF, (size_t)tot * 16, st));
     HIP_TRY(hipMemcpyAsync(e->tm.fx_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
-    if (launch_tm_fx_fill(d, e->tm, e->n, st)) return fail(HTM_E_HIP, "fx fill launch");
+    if (launch_tm_fx_fill(d, e->tm, e->nm, st)) return fail(HTM_E_HIP, "fx fill launch");
     HIP_TRY(hipStreamSynchronize(st));
     e->fx_valid = true;
     return HTM_OK;
@@ -718,8 +735,13 @@ size_t htm_state_bytes(const htm_engine* e, int32_t region) {
     return e->regions[region].per_stream;
 }
 
+// instances of a region: streams, or (model regions of a fleet) the one shared model
+static int32_t region_count(const htm_engine* e, int32_t region) {
+    return e->regions[region].model ? e->nm : e->n;
+}
+
 int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void* h_dst, size_t bytes) {
-    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > e->n)
+    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
         return fail(HTM_E_INVALID, "bad export arguments");
     const Region& r = e->regions[region];
     if (bytes < r.per_stream * n) return fail(HTM_E_INVALID, "export buffer too small");
@@ -729,7 +751,7 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
 }
 
 int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes) {
-    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > e->n)
+    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
         return fail(HTM_E_INVALID, "bad import arguments");
     const Region& r = e->regions[region];
     if (bytes < r.per_stream * n) return fail(HTM_E_INVALID, "import buffer too small");
@@ -778,7 +800,9 @@ int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     for (int id = 1; id <= 16; id++) {
         const Region& r = e->regions[id];
         if (!r.base) continue;
-        if (replicate_region((uint8_t*)r.base, r.per_stream, src, e->n, st)) return fail(HTM_E_HIP, "replicate launch");
+        const int32_t cnt = region_count(e, id);
+        if (cnt < 2) continue;
+        if (replicate_region((uint8_t*)r.base, r.per_stream, src, cnt, st)) return fail(HTM_E_HIP, "replicate launch");
     }
     // SP active list of the last step too (the TM reads it)
     if (replicate_region((uint8_t*)e->sp.act, HTM_MAXACT * 2, src, e->n, st) ||
@@ -788,6 +812,45 @@ int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     e->fx_valid = false;
     return HTM_OK;
 }
+
+int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_streams, int32_t q_capacity,
+                     int32_t device, htm_engine** out) {
+    if (!model || !out || n_streams < 1 || q_capacity < 64) return fail(HTM_E_INVALID, "bad arguments");
+    if (model->fleet) return fail(HTM_E_INVALID, "the model must be an ordinary engine, not a fleet");
+    if (model_stream < 0 || model_stream >= model->n) return fail(HTM_E_INVALID, "bad model stream");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(model->device));
+    HIP_TRY(hipDeviceSynchronize());
+    htm_engine* e = nullptr;
+    int r = create_uninit(&model->cfg, n_streams, device, &e, q_capacity);
+    if (r) return r;
+    // model regions -> the shared instance, per-stream regions -> stream 0 (then every stream)
+    for (int id = 1; id <= 16 && !r; id++) {
+        const Region& src = model->regions[id];
+        const Region& dst = e->regions[id];
+        if (!src.base || !dst.base || src.per_stream != dst.per_stream) {
+            r = fail(HTM_E_STATE, "region %d layout differs", id);
+            break;
+        }
+        if (hipMemcpy(dst.base, (const uint8_t*)src.base + src.per_stream * model_stream, src.per_stream,
+                      hipMemcpyDefault) != hipSuccess)
+            r = fail(HTM_E_HIP, "fleet copy of region %d", id);
+    }
+    if (!r && (hipMemcpy(e->sp.act, model->sp.act + (size_t)model_stream * HTM_MAXACT, HTM_MAXACT * 2,
+                         hipMemcpyDefault) != hipSuccess ||
+               hipMemcpy(e->sp.nact, model->sp.nact + model_stream, 4, hipMemcpyDefault) != hipSuccess))
+        r = fail(HTM_E_HIP, "fleet copy of the SP output");
+    if (!r) r = htm_replicate_stream(e, 0, nullptr);
+    if (r) {
+        htm_destroy(e);
+        return r;
+    }
+    e->sp_learn = e->tm_learn = 0;
+    *out = e;
+    return HTM_OK;
+}
+
+int32_t htm_is_fleet(const htm_engine* e) { return e && e->fleet ? 1 : 0; }
 
 int32_t htm_n_streams(const htm_engine* e) { return e ? e->n : 0; }
 
@@ -821,6 +884,7 @@ int htm_status(htm_engine* e) {
 // save / load: "HTMAMD01", abi, config, n, learning flags, then regions
 int htm_save(htm_engine* e, const char* path) {
     if (!e || !path) return fail(HTM_E_INVALID, "bad arguments");
+    if (e->fleet) return fail(HTM_E_STATE, "fleet engines are not saved: save the model engine they were built from");
     FILE* f = std::fopen(path, "wb");
     if (!f) return fail(HTM_E_IO, "cannot open %s", path);
     const char magic[8] = {'H', 'T', 'M', 'A', 'M', 'D', '0', '1'};

@@ -54,7 +54,13 @@ struct DevCfg {
     int32_t fin_sorted;                   // phase-2 tail: 1 bitonic key sort, 0 column buckets (tuning knob)
     int32_t max_act_cells;                // num_desired * K (frozen collection cell list)
     int32_t n_streams;
+    int32_t shared_model;                 // fleet: every stream reads model instance 0 (SP + TM frozen)
+    int32_t q_cap;                        // per-stream capacity of the qualifying-segment scratch lists
 };
+
+// instance of the model buffers (SP permanences/connections, TM segment
+// pool, frozen index) stream s reads: its own, or the fleet's shared one
+__device__ __forceinline__ int model_stream(const DevCfg& c, int s) { return c.shared_model ? 0 : s; }
 
 // Device buffers (all per-stream strided).
 struct SpBufs {
@@ -84,8 +90,8 @@ struct TmBufs {
     // scratch (per stream)
     uint32_t* scr_bm;       // [S][5][cw]: infA backup, infP(t-1) backup, infA cand, infP cand, spare
     float* scr_conf;        // [S][ncol]: colConf candidate
-    uint32_t* scr_q;        // [S][seg_cap]: qualifying segment keys
-    uint32_t* scr_q2;       // [S][seg_cap]: bucket-sorted keys
+    uint32_t* scr_q;        // [S][q_cap]: qualifying segment keys
+    uint32_t* scr_q2;       // [S][q_cap] (>= seg_cap entries): bucket-sorted keys / index-build pid map
     uint8_t* prev_pred;     // [S][ncol] nonzero(colConf(t-1)) captured before compute
     uint32_t* scr_cur;      // [S][ncells*fx_nwin] frozen-index fill cursors
     // frozen forward index (valid while TM learning is off): for stream s,

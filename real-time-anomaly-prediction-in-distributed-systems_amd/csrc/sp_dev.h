@@ -43,7 +43,7 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     uint32_t p0[HTM_NPLANES], p1[HTM_NPLANES];
 #pragma unroll
     for (int k = 0; k < HTM_NPLANES; k++) { p0[k] = 0; p1[k] = 0; }
-    const uint32_t* connT = b.connT + (size_t)s * c.nin_pad * nw;
+    const uint32_t* connT = b.connT + (size_t)model_stream(c, s) * c.nin_pad * nw;
     const int nai = sh.n_act_inputs;
     for (int a = 0; a < nai; a++) {
         const uint32_t* row = connT + (size_t)sh.act_inputs[a] * nw;
@@ -151,9 +151,10 @@ __device__ __forceinline__ float sp_update_perm(const DevCfg& c, float p, bool r
 __device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b, int s, int col, const uint32_t* in_bits, int mode) {
     const int l = lane_id();
     const int pw = c.nin_pad >> 5;
-    const uint32_t* prow = b.potmask + ((size_t)s * c.ncol + col) * pw;
-    float* perm = b.perm + ((size_t)s * c.ncol + col) * c.n_potential;
-    uint32_t* connT = b.connT + (size_t)s * c.nin_pad * c.nw;
+    const size_t ms = (size_t)model_stream(c, s);
+    const uint32_t* prow = b.potmask + (ms * c.ncol + col) * pw;
+    float* perm = b.perm + (ms * c.ncol + col) * c.n_potential;
+    uint32_t* connT = b.connT + ms * c.nin_pad * c.nw;
     const uint32_t cw = (uint32_t)col >> 5, cb = 1u << (col & 31);
     int rank_base = 0;
     for (int chunk = 0; chunk < pw; chunk += 16) {  // 16 words = 512 inputs per pass
@@ -222,7 +223,7 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     for (int a = wave_id(); a < nact; a += blockDim.x >> 6) sp_adapt_column(c, b, s, sh.actlist[a], sh.in, 0);
     __syncthreads();
     // ---- updateDutyCycles_ (period = min(dutyCyclePeriod, iterationNum))
-    float* odc = b.duty + (size_t)s * 2 * c.ncol;
+    float* odc = b.duty + (size_t)model_stream(c, s) * 2 * c.ncol;
     float* adc = odc + c.ncol;
     const uint32_t period = (uint32_t)c.dc_period > sh.iter ? sh.iter : (uint32_t)c.dc_period;
     const float pm1 = (float)(period - 1), pf = (float)period;

@@ -336,7 +336,10 @@ __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int t
     const uint32_t sub = threadIdx.x & 3;
     uint32_t nb = scan_pool(t, state, [](uint32_t) { return true; },
                             [&](uint32_t slot, uint32_t, bool el, uint32_t mask) {
-                                if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) t.q1[atomicAdd(&t.sh->qn, 1)] = slot;
+                                if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) {
+                                    const uint32_t i = (uint32_t)atomicAdd(&t.sh->qn, 1);
+                                    if (i < (uint32_t)t.c.q_cap) t.q1[i] = slot;
+                                }
                             });
     nb = wg_sum(t.sh, nb);
     if (threadIdx.x == 0) t.sh->bytes += nb;
@@ -358,7 +361,7 @@ __device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v) {
 // only grow) appends base + slot to dst at *qn -- qualification without a
 // sweep over the counters
 __device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint32_t thr, uint32_t base, int32_t* qn,
-                                                    uint32_t* dst) {
+                                                    uint32_t* dst, uint32_t qcap) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t old[8];
 #pragma unroll
@@ -369,7 +372,10 @@ __device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint
 #pragma unroll
     for (int h = 0; h < 8; h++) {
         const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) dst[atomicAdd(qn, 1)] = base + rel;
+        if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) {
+            const uint32_t i = (uint32_t)atomicAdd(qn, 1);
+            if (i < qcap) dst[i] = base + rel;
+        }
     }
 }
 
@@ -382,7 +388,8 @@ __device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint
 template <bool PUSH>
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
                                           uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t thr = 0,
-                                          uint32_t base = 0, int32_t* qn = nullptr, uint32_t* dst = nullptr) {
+                                          uint32_t base = 0, int32_t* qn = nullptr, uint32_t* dst = nullptr,
+                                          uint32_t qcap = 0) {
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
         for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
@@ -403,7 +410,7 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
         }
 #pragma unroll
         for (int j = 0; j < FX_DEPTH; j++) {
-            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst);
+            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap);
             else fx_count_block(cnt, v[j]);
         }
         __syncthreads();
@@ -552,7 +559,9 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         COUNT(t, SC_WIN, 1);
         COUNT(t, SC_BLK, B);
         if (w < 0) fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner);
-        else fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, (uint32_t)thr, (uint32_t)w * W, &sh->qn, t.q1);
+        else
+            fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, (uint32_t)thr, (uint32_t)w * W, &sh->qn, t.q1,
+                            (uint32_t)c.q_cap);
         STAMP(t, SB_STREAM);
         if (w < 0) {
             // pid counter >= activationThreshold: the segment's cell is predicted
@@ -850,6 +859,11 @@ __device__ __forceinline__ bool infer_phase2(Tm& t) {
     __syncthreads();
     if (FROZEN) collect_frozen(t, t.c.act_thr);
     else collect_scan(t, t.infA, t.c.act_thr);
+    __syncthreads();
+    if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)t.c.q_cap) {
+        sh->err |= 16u;  // qualifying-segment list overflow (fleet q_capacity): results invalid
+        sh->qn = t.c.q_cap;
+    }
     __syncthreads();
     uint32_t npc = phase2_finish<FROZEN>(t);
     return (double)npc >= 0.5 * sh->avg_dens;
@@ -1641,23 +1655,27 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     t.flags = reinterpret_cast<uint32_t*>(lds + L.off_flags);
     t.U = reinterpret_cast<uint32_t*>(lds + L.off_U);
     const size_t sc = (size_t)c.seg_cap;
-    t.meta = b.seg_meta + (size_t)s * sc;
-    t.src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
-    t.perm = b.seg_perm + (size_t)s * sc * HTM_MAXSYN;
-    t.conn = b.seg_conn + (size_t)s * sc;
-    t.duty = b.seg_duty + (size_t)s * sc * 3;
-    t.nseg = b.cell_nseg + (size_t)s * c.ncells;
-    t.upd = b.upd + (size_t)s * c.upd_cap;
+    // model buffers: the stream's own, or the fleet's shared instance 0
+    // (frozen inference writes only the segments' dutyCycle cache, with the
+    // value every stream computes for it, so sharing is race-free)
+    const size_t ms = (size_t)model_stream(c, s);
+    t.meta = b.seg_meta + ms * sc;
+    t.src = b.seg_src + ms * sc * HTM_MAXSYN;
+    t.perm = b.seg_perm + ms * sc * HTM_MAXSYN;
+    t.conn = b.seg_conn + ms * sc;
+    t.duty = b.seg_duty + ms * sc * 3;
+    t.nseg = b.cell_nseg + ms * c.ncells;
+    t.upd = b.upd + ms * c.upd_cap;
     t.sbm = b.scr_bm + (size_t)s * 5 * c.cw;
     t.sconf = b.scr_conf + (size_t)s * c.ncol;
-    t.q1 = b.scr_q + (size_t)s * sc;
-    t.q2 = b.scr_q2 + (size_t)s * sc;
+    t.q1 = b.scr_q + (size_t)s * c.q_cap;
+    t.q2 = b.scr_q2 + (size_t)s * c.q_cap;
     if (FROZEN) {
-        t.fxoff = b.fx_off + (size_t)s * (size_t)c.fx_noff;
-        t.fxent = b.fx_ent + b.fx_base[s];
-        t.fxrec = b.fx_rec + (size_t)s * sc;
-        t.fxpcell = b.fx_pcell + (size_t)s * c.fx_pcap;
-        t.np = b.fx_np[s];
+        t.fxoff = b.fx_off + ms * (size_t)c.fx_noff;
+        t.fxent = b.fx_ent + b.fx_base[ms];
+        t.fxrec = b.fx_rec + ms * sc;
+        t.fxpcell = b.fx_pcell + ms * c.fx_pcap;
+        t.np = b.fx_np[ms];
     } else {
         t.fxoff = nullptr;
         t.fxent = nullptr;
@@ -1852,8 +1870,13 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
 // stream never waits for the others between steps (streams are
 // independent; every stream's result is the one per-step launches give).
 // The SP's LDS aliases the TM union region, which is free between steps.
+#ifdef HTM_RUN_WAVES
+#define HTM_RUN_ATTR __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES)))
+#else
+#define HTM_RUN_ATTR
+#endif
 template <bool LEARN, bool FROZEN>
-__global__ __launch_bounds__(TM_NT) void htm_run_kernel(DevCfg c, TmBufs b, SpBufs sp, const double* values,
+__global__ __launch_bounds__(TM_NT) HTM_RUN_ATTR void htm_run_kernel(DevCfg c, TmBufs b, SpBufs sp, const double* values,
                                                         float* scores, int n_steps, int sp_learn, int keep_prev,
                                                         int keep_overlaps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];

@@ -50,6 +50,26 @@ class HTMEngine:
         self.sp_learn = True
         self.tm_learn = True
         self.fused = os.environ.get("HTM_FUSED", "1") != "0"  # the engine's default (HTM_OPT_FUSED)
+        self.is_fleet = bool(self._L.htm_is_fleet(self.h))
+        if self.is_fleet:
+            self.sp_learn = self.tm_learn = False
+
+    @classmethod
+    def fleet(cls, model: "HTMEngine", n_streams: int, model_stream: int = 0, q_capacity: int = 8192,
+              device: int | None = None) -> "HTMEngine":
+        """Fleet mode (config 4): n_streams streams sharing the frozen SP+TM model
+        of `model`'s stream `model_stream`, each with its own TM state."""
+        L = _lib.lib()
+        dev = model.device if device is None else int(device)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(L.htm_create_fleet(model.h, int(model_stream), int(n_streams), int(q_capacity), dev,
+                                     ctypes.byref(h)))
+        return cls(0, device=dev, _handle=h)
+
+    def _model_index(self, s: int) -> int:
+        """instance of the model regions stream s reads (fleet: the shared one)"""
+        return 0 if self.is_fleet else s
 
     # ------------------------------------------------------------------ life
     def close(self):
@@ -225,16 +245,16 @@ class HTMEngine:
         nin = c.n_fields * c.enc_n
         nin_pad = (nin + 31) // 32 * 32
         nw = c.sp_columns // 32
-        pot_words = self.export_state("sp_potmask", s, 1)[0].view(np.uint32).reshape(c.sp_columns, nin_pad // 32)
+        pot_words = self.export_state("sp_potmask", self._model_index(s), 1)[0].view(np.uint32).reshape(c.sp_columns, nin_pad // 32)
         pot = np.unpackbits(pot_words.view(np.uint8).reshape(c.sp_columns, -1), axis=1, bitorder="little")[:, :nin]
-        packed = self.export_state("sp_perm", s, 1)[0].view(np.float32).reshape(c.sp_columns, -1)
+        packed = self.export_state("sp_perm", self._model_index(s), 1)[0].view(np.float32).reshape(c.sp_columns, -1)
         perm = np.zeros((c.sp_columns, nin), np.float32)
         for col in range(c.sp_columns):
             idx = np.nonzero(pot[col])[0]
             perm[col, idx] = packed[col, : len(idx)]
-        connT = self.export_state("sp_connT", s, 1)[0].view(np.uint32).reshape(nin_pad, nw)
+        connT = self.export_state("sp_connT", self._model_index(s), 1)[0].view(np.uint32).reshape(nin_pad, nw)
         conn = np.unpackbits(connT.view(np.uint8).reshape(nin_pad, -1), axis=1, bitorder="little")[:nin, :c.sp_columns]
-        duty = self.export_state("sp_duty", s, 1)[0].view(np.float32).reshape(2, c.sp_columns)
+        duty = self.export_state("sp_duty", self._model_index(s), 1)[0].view(np.float32).reshape(2, c.sp_columns)
         sc = self.export_state("sp_scalars", s, 1)[0].view(np.uint32)
         return dict(perm=perm, potential=pot.astype(np.uint8), connected=conn.T.copy().astype(np.uint8),
                     overlap_dc=duty[0].copy(), active_dc=duty[1].copy(),
@@ -243,7 +263,7 @@ class HTMEngine:
     def tm_segments(self, s: int) -> dict:
         """Live segments of stream s in canonical (cell, creation) order, the
         layout of oracle.OracleModel.tm_segments(32)."""
-        meta = self.export_state("tm_seg_meta", s, 1)[0].view(np.uint32)
+        meta = self.export_state("tm_seg_meta", self._model_index(s), 1)[0].view(np.uint32)
         hdr = self.tm_header(s)
         hwm = hdr.seg_hwm
         meta = meta[:hwm]
@@ -253,9 +273,9 @@ class HTMEngine:
         order = np.lexsort((slots, cell))
         slots = slots[order]
         m = meta[slots]
-        src = self.export_state("tm_seg_src", s, 1)[0].view(np.uint16).reshape(-1, 32)[slots].astype(np.int32)
-        perm = self.export_state("tm_seg_perm", s, 1)[0].view(np.float32).reshape(-1, 32)[slots]
-        duty = self.export_state("tm_seg_duty", s, 1)[0].view(np.uint32).reshape(-1, 3)[slots]
+        src = self.export_state("tm_seg_src", self._model_index(s), 1)[0].view(np.uint16).reshape(-1, 32)[slots].astype(np.int32)
+        perm = self.export_state("tm_seg_perm", self._model_index(s), 1)[0].view(np.float32).reshape(-1, 32)[slots]
+        duty = self.export_state("tm_seg_duty", self._model_index(s), 1)[0].view(np.uint32).reshape(-1, 3)[slots]
         nsyn = ((m >> 16) & 0x3F).astype(np.int32)
         mask = np.arange(32)[None, :] < nsyn[:, None]
         return dict(cell=(m & 0xFFFF).astype(np.int32), is_seq=((m >> 22) & 1).astype(np.int32),

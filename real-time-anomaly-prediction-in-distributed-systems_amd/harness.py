@@ -89,6 +89,53 @@ class SLOHarness:
         return out
 
 
+class AnomalyLikelihood:
+    """NuPIC's AnomalyLikelihood.anomalyProbability for N streams at once on
+    the GPU (csrc/likelihood.hip; parity unpinned -- the reference has no
+    likelihood).  Defaults are NuPIC's."""
+
+    def __init__(self, n_streams: int, learning_period: int = 288, estimation_samples: int = 100,
+                 historic_window: int = 8640, reestimation_period: int = 100, device: int | None = None):
+        import torch
+        self._L = _lib.lib()
+        self.n_streams = int(n_streams)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        check(self._L.htm_likelihood_create(self.n_streams, int(learning_period), int(estimation_samples),
+                                            int(historic_window), int(reestimation_period), self.device,
+                                            ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.htm_likelihood_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def anomaly_probability(self, values, scores, out=None):
+        """values: device float64 [n_streams] or [n_streams, fields] (field 0 is
+        the metric); scores: device float32 [n_streams].  Returns float64 [n]."""
+        import torch
+        v = values.contiguous()
+        stride = 1 if v.dim() == 1 else v.shape[1]
+        if v.dtype != torch.float64 or v.shape[0] != self.n_streams:
+            raise ValueError("values must be float64 [n_streams(, fields)]")
+        sc = scores.contiguous()
+        if sc.dtype != torch.float32 or sc.numel() != self.n_streams:
+            raise ValueError("scores must be float32 [n_streams]")
+        if out is None:
+            out = torch.empty(self.n_streams, dtype=torch.float64, device=sc.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        check(self._L.htm_likelihood_step(self.h, ctypes.c_void_p(v.data_ptr()), int(stride),
+                                          ctypes.c_void_p(sc.data_ptr()), ctypes.c_void_p(out.data_ptr()), st))
+        return out
+
+
 def valid_records(cpu, mem):
     """ModelTraining.py:29-32 / ModelTesting.py:51-53: a record with a null cpu
     or mem is skipped."""

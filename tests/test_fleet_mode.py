@@ -1,0 +1,70 @@
+"""Fleet mode (config 4): streams sharing one frozen SP+TM model give exactly
+the results of an ordinary engine holding a copy of the model per stream."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+
+@pytest.fixture(scope="module")
+def model(rt, traces):
+    eng = rt.HTMEngine(1, seg_capacity=1 << 15)
+    eng.run(torch.tensor(traces["train"][:500], dtype=torch.float64, device="cuda").reshape(-1, 1))
+    eng.status()
+    return eng
+
+
+def replicas(rt, model, n):
+    eng = rt.HTMEngine(n, seg_capacity=1 << 15)
+    for region in rt._lib.ST:
+        eng.import_state(region, model.export_state(region, 0, 1), s0=0)
+    eng.replicate(0)
+    eng.set_learning(False, False)
+    return eng
+
+
+@pytest.mark.parametrize("frozen", [True, False])
+def test_fleet_equals_replicated_engines(rt, model, traces, frozen):
+    n, T = 16, 120
+    rep = replicas(rt, model, n)
+    fl = rt.HTMEngine.fleet(model, n, q_capacity=4096)
+    assert fl.is_fleet and fl.device_bytes() < rep.device_bytes() / 4
+    for e in (rep, fl):
+        e.use_frozen_index(frozen)
+    rng = np.random.default_rng(17)
+    base = np.asarray(traces["test"][:T], np.float64)
+    vals = np.clip(base[:, None] + rng.integers(-3, 4, size=(T, n)), 0, 100)
+    vals[rng.random(vals.shape) < 0.02] = np.nan
+    v = torch.tensor(vals, device="cuda")
+    a = rep.run(v).cpu().numpy()
+    b = fl.run(v[:60]).cpu().numpy()
+    b = np.concatenate([b, np.stack([fl.step(v[k]).cpu().numpy() for k in range(60, T)])])
+    assert np.array_equal(a, b)
+    for s in [0, n - 1]:
+        sa, sb = rep.tm_states(s), fl.tm_states(s)
+        for k in sa:
+            assert np.array_equal(sa[k], sb[k])
+        assert np.array_equal(rep.col_confidence(s), fl.col_confidence(s))
+    # the shared model is read-only except for the segments' dutyCycle cache:
+    # at the frozen iteration, Segment::dutyCycle() stores the value it
+    # returns, so the fleet's cache holds the updates of every stream and
+    # stream 0's replica only its own -- entries differ only where the
+    # fleet's was refreshed at the frozen iteration (outputs are unaffected)
+    ga, gb = rep.tm_segments(0), fl.tm_segments(0)
+    for k in ["cell", "nsyn", "src", "perm", "pos_act"]:
+        assert np.array_equal(ga[k], gb[k])
+    it = fl.tm_header(0).lrn_iter
+    diff = (ga["last_dc"] != gb["last_dc"]) | (ga["last_dc_iter"] != gb["last_dc_iter"])
+    assert np.all(gb["last_dc_iter"][diff] == it)
+    fl.status()
+
+
+def test_fleet_refuses_learning_and_save(rt, model, tmp_path):
+    fl = rt.HTMEngine.fleet(model, 4)
+    with pytest.raises(rt.HtmError):
+        fl.set_learning(True, False)
+    with pytest.raises(rt.HtmError):
+        fl.save(str(tmp_path / "f.htm"))
