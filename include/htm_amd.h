@@ -136,9 +136,9 @@ int htm_counters(htm_engine* eng, uint64_t* out8);
 
 /* Diagnostic builds only (libhtm_amd_stamps.so, -DHTM_STAMPS): per-phase
  * shader-cycle stamps of the TM kernel summed over streams since the last
- * call (out32[0..15]) and event counts (out32[16..31]); HTM_E_STATE in the
+ * call (out48[0..23]) and event counts (out48[24..47]); HTM_E_STATE in the
  * product library. */
-int htm_debug_stamps(htm_engine* eng, uint64_t* out32);
+int htm_debug_stamps(htm_engine* eng, uint64_t* out48);
 
 /* Synchronise and check every stream's overflow flags (HTM_E_CAPACITY). */
 int htm_status(htm_engine* eng);

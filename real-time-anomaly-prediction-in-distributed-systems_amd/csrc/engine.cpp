@@ -225,7 +225,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // fill the LDS budget (two workgroups per CU by default).  Out-list
     // entries are window-relative u16 with 0xFFFF as padding.
     const size_t off_u = tm_step_lds_base(d, 0, 1);
-    const size_t cell_words = (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1 + FX_OWN / 2;
+    const size_t cell_words = 4 + (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1 + FX_OWN / 2;
     size_t avail = lds_budget > off_u ? (lds_budget - off_u) / 4 : 0;
     size_t win = avail > cell_words ? (avail - cell_words) * 4 : 0;
     win = (win / 1024) * 1024;
@@ -292,7 +292,7 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
-    ALLOC(e->tm.dbg, uint64_t, S * 32);
+    ALLOC(e->tm.dbg, uint64_t, S * 2 * HTM_NSTAMP);
 #endif
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
@@ -606,15 +606,16 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
     return HTM_OK;
 }
 
-int htm_debug_stamps(htm_engine* e, uint64_t* out32) {
-    if (!e || !out32) return fail(HTM_E_INVALID, "bad arguments");
+int htm_debug_stamps(htm_engine* e, uint64_t* out48) {
+    if (!e || !out48) return fail(HTM_E_INVALID, "bad arguments");
     if (!e->tm.dbg) return fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
     HIP_TRY(hipDeviceSynchronize());
-    std::vector<uint64_t> h((size_t)e->n * 32);
+    const int W = 2 * HTM_NSTAMP;
+    std::vector<uint64_t> h((size_t)e->n * W);
     HIP_TRY(hipMemcpy(h.data(), e->tm.dbg, h.size() * 8, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 32; k++) out32[k] = 0;
+    for (int k = 0; k < W; k++) out48[k] = 0;
     for (int s = 0; s < e->n; s++)
-        for (int k = 0; k < 32; k++) out32[k] += h[(size_t)s * 32 + k];
+        for (int k = 0; k < W; k++) out48[k] += h[(size_t)s * W + k];
     HIP_TRY(hipMemset(e->tm.dbg, 0, h.size() * 8));
     return HTM_OK;
 }

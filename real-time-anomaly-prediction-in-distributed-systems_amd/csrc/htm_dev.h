@@ -18,11 +18,17 @@
 #define HTM_MAXPAT 16     // backtrack pattern history slots
 #define HTM_NPLANES 7     // bit-sliced overlap planes (overlap <= 127)
 #define HTM_MAXNW 128     // ncol/32 words (ncol <= 4096)
+#ifndef TM_NT
 #define TM_NT 256                  // threads of the TM workgroup (one stream)
+#endif
 #define TM_NWAVES (TM_NT / 64)
 #define FX_DEPTH 8                 // frozen index: out-list blocks in flight per thread
 #define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
-#define FX_MAXPER 8                // active cells per thread (<= 64 columns x 32 cells / TM_NT)
+#define FX_MAXPER ((HTM_MAXACT * HTM_MAXK + TM_NT - 1) / TM_NT)  // active cells per thread
+#ifndef HTM_FX_PUSH
+#define HTM_FX_PUSH 1              // 1: qualify segments as their counters reach the threshold (returning
+                                   //    LDS atomics); 0: count with plain atomics, then sweep the counters
+#endif
 
 // Derived, immutable engine constants (kernel argument).
 struct DevCfg {
@@ -118,7 +124,7 @@ struct TmBufs {
 // Diagnostic phase stamps (HTM_STAMPS builds only): thread 0 charges the
 // shader cycles since its previous stamp to bucket k.  Compiled out of the
 // product library.
-#define HTM_NSTAMP 16
+#define HTM_NSTAMP 24  // stamp buckets; the debug record per stream is 2 x HTM_NSTAMP words
 #ifdef HTM_STAMPS
 #define STAMP(t, k)                                                     \
     do {                                                                \
@@ -132,9 +138,18 @@ struct TmBufs {
     do {                                                                \
         if (threadIdx.x == 0) (t).sh->st_cnt[(k)] += (uint64_t)(v);     \
     } while (0)
+#define STAMP_SH(sh, k)                                                 \
+    do {                                                                \
+        if (threadIdx.x == 0) {                                         \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();         \
+            (sh)->st_acc[(k)] += now_ - (sh)->st_last;                  \
+            (sh)->st_last = now_;                                       \
+        }                                                               \
+    } while (0)
 #else
 #define STAMP(t, k) do { } while (0)
 #define COUNT(t, k, v) do { } while (0)
+#define STAMP_SH(sh, k) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------

@@ -34,7 +34,7 @@ struct SpShared {
     uint32_t iter;
     int32_t nbump;
     uint16_t bump[HTM_MAXNW * 32 > 4096 ? 4096 : HTM_MAXNW * 32];
-    float red[4];
+    float red[16];  // per-wave maxima (<= 16 waves)
 };
 
 __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SpShared& sh, int write_overlaps) {

@@ -35,7 +35,8 @@ __constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 10000
 
 struct __attribute__((aligned(16))) TmSh {
     double avg_dens, avg_lsl;
-    unsigned long long bytes;  // algorithmic HBM bytes of this step (thread 0 / LDS atomics)
+    unsigned long long bytes;      // algorithmic HBM bytes of this step (thread 0 / LDS atomics)
+    unsigned long long bytes_acc;  // ... of the earlier steps of a run kept in LDS
     uint32_t lrn_iter, iter;
     int32_t pam, lsl, reset, have_avg;
     uint32_t rng[31];
@@ -93,7 +94,7 @@ struct Tm {
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS
+    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -132,8 +133,8 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
                  (size_t)(c.q_lds + 1) / 2;
     size_t keys = learn ? 2 * (size_t)c.ncol : 0;
-    size_t col = frozen ? (size_t)c.fx_win / 4 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells + 1 +
-                              FX_OWN / 2
+    size_t col = frozen ? (size_t)c.fx_win / 4 + 4 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
+                              1 + FX_OWN / 2
                         : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
     size_t spw = (sizeof(SpShared) + 3) / 4;  // the fused kernels' SP step
@@ -348,12 +349,37 @@ __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int t
 
 // one 16-byte block of a frozen out-list: 8 window-relative u16 slots,
 // 0xFFFF = padding; bump the slot's u8 counter
-__device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v) {
+// (padding is counted branch-free into the spare word cnt[dummy] past the counters)
+__device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v, uint32_t dummy) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int h = 0; h < 8; h++) {
         const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        if (rel != 0xFFFFu) atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
+        atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy], 1u << ((rel & 3) * 8));
+    }
+}
+
+// Every counter byte >= thr of cnt[0 .. nbytes) (nbytes a multiple of 16) as
+// slot base + index appended to dst at *qn (dense sweep after counting with
+// non-returning atomics; HTM_FX_PUSH=0 builds).
+__device__ __forceinline__ void fx_collect_dense(const uint32_t* cnt, uint32_t nbytes, uint32_t thr, uint32_t base,
+                                                 int32_t* qn, uint32_t* dst, uint32_t qcap) {
+    const uint32_t add = 0x01010101u * (128u - thr);
+    const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
+    const uint32_t n16 = nbytes / 16;
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < n16; i += TM_NT) {
+        const uint4 x = c4[i];
+        uint32_t m[4] = {(x.x + add) & 0x80808080u, (x.y + add) & 0x80808080u, (x.z + add) & 0x80808080u,
+                         (x.w + add) & 0x80808080u};
+        if ((m[0] | m[1] | m[2] | m[3]) == 0u) continue;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            for (uint32_t y = m[q]; y; y &= y - 1) {
+                const uint32_t k = (uint32_t)atomicAdd(qn, 1);
+                if (k < qcap) dst[k] = base + 16 * i + 4 * q + ((__ffs(y) - 1) >> 3);
+            }
+        }
     }
 }
 
@@ -387,9 +413,9 @@ __device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint
 // FX_OWN blocks whatever the list lengths.
 template <bool PUSH>
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
-                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t thr = 0,
+                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy, uint32_t thr = 0,
                                           uint32_t base = 0, int32_t* qn = nullptr, uint32_t* dst = nullptr,
-                                          uint32_t qcap = 0) {
+                                          uint32_t qcap = 0, TmSh* shp = nullptr) {
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
         for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
@@ -398,6 +424,7 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
             for (uint32_t x = a; x < z; x++) owner[x - lo] = (uint16_t)k;
         }
         __syncthreads();
+        STAMP_SH(shp, SB_OWNER);
         uint4 v[FX_DEPTH];
 #pragma unroll
         for (int j = 0; j < FX_DEPTH; j++) {
@@ -410,9 +437,16 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
         }
 #pragma unroll
         for (int j = 0; j < FX_DEPTH; j++) {
+#ifdef HTM_STAMPS
+            if (j == 0 && threadIdx.x == 0) {
+                __builtin_amdgcn_s_waitcnt(0);  // diagnostic: charge the block loads' latency to SB_SLOAD
+                STAMP_SH(shp, SB_SLOAD);
+            }
+#endif
             if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap);
-            else fx_count_block(cnt, v[j]);
+            else fx_count_block(cnt, v[j], dummy);
         }
+        STAMP_SH(shp, SB_COUNT);
         __syncthreads();
     }
 }
@@ -496,9 +530,10 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     TmSh* sh = t.sh;
     const uint32_t W = (uint32_t)c.fx_win;
     const uint32_t mac = (uint32_t)c.max_act_cells;
-    uint32_t* cnt = t.U;
-    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4);
-    uint32_t* pstart = t.U + W / 4 + (mac + 1) / 2;
+    uint32_t* cnt = t.U;  // W / 4 counter words + 4 spare (padding sink)
+    const uint32_t dummy = W / 4;
+    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4 + 4);
+    uint32_t* pstart = t.U + W / 4 + 4 + (mac + 1) / 2;
     uint32_t* plo = pstart + mac + 1;
     uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
     const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
@@ -558,11 +593,20 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         STAMP(t, SB_WINPRE);
         COUNT(t, SC_WIN, 1);
         COUNT(t, SC_BLK, B);
-        if (w < 0) fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner);
+#if HTM_FX_PUSH
+        if (w < 0) fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, 0, 0, nullptr, nullptr, 0, sh);
         else
-            fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, (uint32_t)thr, (uint32_t)w * W, &sh->qn, t.q1,
-                            (uint32_t)c.q_cap);
+            fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, (uint32_t)thr, (uint32_t)w * W, &sh->qn,
+                            t.q1, (uint32_t)c.q_cap, sh);
         STAMP(t, SB_STREAM);
+#else
+        fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, 0, 0, nullptr, nullptr, 0, sh);
+        STAMP(t, SB_STREAM);
+        if (w >= 0) {
+            fx_collect_dense(cnt, nbytes, (uint32_t)thr, (uint32_t)w * W, &sh->qn, t.q1, (uint32_t)c.q_cap);
+            __syncthreads();
+        }
+#endif
         if (w < 0) {
             // pid counter >= activationThreshold: the segment's cell is predicted
             const uint32_t np = t.np;
@@ -1636,8 +1680,12 @@ __device__ __forceinline__ void compact_pool(Tm& t) {
 // One BacktrackingTM.compute + raw anomaly of stream s by the calling
 // workgroup (TM_NT threads), LDS at `lds` (tm_layout).
 template <bool LEARN, bool FROZEN>
+// first / last: the step opens / closes a run of steps by this workgroup.
+// Between them the stream's TM state (cell bitmaps, colConfidence, header,
+// pattern history, RNG) stays in LDS: only the first step loads it from HBM
+// and only the last writes it back.
 __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores,
-                                             int keep_prev, int s, uint8_t* lds) {
+                                             int keep_prev, int s, uint8_t* lds, int first = 1, int last = 1) {
     const TmLayout L = tm_layout(c, LEARN, FROZEN);
     Tm t;
     t.c = c;
@@ -1696,7 +1744,24 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     float* gconf = b.colconf + (size_t)s * c.ncol;
     uint16_t* gpat = b.pat + (size_t)s * 2 * HTM_MAXPAT * HTM_MAXACT;
     // ---- load state
-    if (threadIdx.x == 0) {
+    if (!first) {
+        // continuing in LDS: t -> t-1 rotation of the predicted / learn states
+        if (threadIdx.x == 0) {
+            const uint32_t na = sp.nact[s];
+            sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
+            sh->bytes = 4ull;
+        }
+        if (threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
+        wg_copy(t.infP1, t.infP, c.cw);
+        if (LEARN) {
+            wg_copy(t.lrnA1, t.lrnA, c.cw);
+            wg_copy(t.lrnP1, t.lrnP, c.cw);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) sh->bytes += 2ull * sh->nA;
+    }
+    if (first && threadIdx.x == 0) {
+        sh->bytes_acc = 0;
         sh->avg_dens = hdr->avg_input_density;
         sh->avg_lsl = hdr->avg_learned_seq_length;
         sh->lrn_iter = hdr->lrn_iter;
@@ -1722,15 +1787,15 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         uint32_t na = sp.nact[s];
         sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
     }
-    if (threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
-    if (threadIdx.x < HTM_MAXPAT) {
+    if (first && threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
+    if (first && threadIdx.x < HTM_MAXPAT) {
         sh->inf_len[threadIdx.x] = hdr->inf_pat_len[threadIdx.x];
         sh->lrn_len[threadIdx.x] = hdr->lrn_pat_len[threadIdx.x];
     }
-    if (threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
+    if (first && threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
     __syncthreads();
     // live pattern-history entries only (ring slots head .. head+n-1)
-    {
+    if (first) {
         const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
         for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
             const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
@@ -1752,22 +1817,26 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
                         (LEARN ? 3ull : 1ull) * 4ull * c.cw + 4ull * sh->nA;
         }
     }
-    wg_copy(t.infP1, gbm + c.cw, c.cw);   // infPredictedState t -> t-1
-    wg_copy(t.infP, gbm + c.cw, c.cw);
-    if (LEARN) {
-        wg_copy(t.lrnA1, gbm + 2 * c.cw, c.cw);  // lrnActiveState t -> t-1
-        wg_copy(t.lrnP1, gbm + 3 * c.cw, c.cw);  // lrnPredictedState t -> t-1
-        wg_copy(t.lrnA, gbm + 2 * c.cw, c.cw);
-        wg_copy(t.lrnP, gbm + 3 * c.cw, c.cw);
+    if (first) {
+        wg_copy(t.infP1, gbm + c.cw, c.cw);  // infPredictedState t -> t-1
+        wg_copy(t.infP, gbm + c.cw, c.cw);
+        if (LEARN) {
+            wg_copy(t.lrnA1, gbm + 2 * c.cw, c.cw);  // lrnActiveState t -> t-1
+            wg_copy(t.lrnP1, gbm + 3 * c.cw, c.cw);  // lrnPredictedState t -> t-1
+            wg_copy(t.lrnA, gbm + 2 * c.cw, c.cw);
+            wg_copy(t.lrnP, gbm + 3 * c.cw, c.cw);
+        }
     }
     __syncthreads();
     const int nA = sh->nA;
-    // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1))
+    // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1)),
+    // from HBM on the first step of a run, from LDS after it
+    const float* pconf = first ? gconf : t.colconf;
     uint32_t hit = 0;
-    for (int a = threadIdx.x; a < nA; a += TM_NT) hit += gconf[sh->act[a]] != 0.0f ? 1u : 0u;
+    for (int a = threadIdx.x; a < nA; a += TM_NT) hit += pconf[sh->act[a]] != 0.0f ? 1u : 0u;
     if (keep_prev)
         for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
-            b.prev_pred[(size_t)s * c.ncol + col] = gconf[col] != 0.0f ? 1 : 0;
+            b.prev_pred[(size_t)s * c.ncol + col] = pconf[col] != 0.0f ? 1 : 0;
     hit = wg_sum(sh, hit);
     if (threadIdx.x == 0) {
         // computeRawAnomalyScore -> Real32 output
@@ -1789,8 +1858,31 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     STAMP(t, SB_BT);
     if (LEARN) update_learning(t);
     STAMP(t, SB_LEARN);
-    // ---- write back
+    // ---- write back (last step of the run only)
     __syncthreads();
+    if (!last) {
+        if (threadIdx.x == 0) {
+            sh->bytes_acc += sh->bytes;
+            sh->reset = 0;  // reset_called is consumed by the step after the reset
+        }
+#ifdef HTM_STAMPS
+        __syncthreads();
+        STAMP(t, SB_WB);
+        COUNT(t, SC_STEPS, 1);
+        if (threadIdx.x == 0) {
+            uint64_t x = (sh->st_last - sh->st_start) >> 16;
+            int hb = 0;
+            while (x && hb < 8) { hb++; x >>= 1; }
+            sh->st_cnt[SC_HIST + hb] += 1;
+            uint64_t* d = b.dbg + (size_t)s * 2 * HTM_NSTAMP;
+            for (int k = 0; k < HTM_NSTAMP; k++) {
+                d[k] += sh->st_acc[k];
+                d[HTM_NSTAMP + k] += sh->st_cnt[k];
+            }
+        }
+#endif
+        return;
+    }
     wg_copy(gbm, t.infA, c.cw);
     wg_copy(gbm + c.cw, t.infP, c.cw);
     if (LEARN) {
@@ -1798,17 +1890,32 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
     }
     wg_copy(reinterpret_cast<uint32_t*>(gconf), reinterpret_cast<const uint32_t*>(t.colconf), c.ncol);
-    // patterns only change by the push of this step (pops move the heads)
-    if (sh->ti[0] >= 0)
-        for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
-            gpat[sh->ti[0] * HTM_MAXACT + a] = sh->inf_pat[sh->ti[0]][a];
-    if (LEARN && sh->ti[1] >= 0)
-        for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
-            gpat[(HTM_MAXPAT + sh->ti[1]) * HTM_MAXACT + a] = sh->lrn_pat[sh->ti[1]][a];
+    // patterns: a single step changes only the slot it pushed (pops move
+    // the heads); a run of steps writes back every live slot
+    if (first) {
+        if (sh->ti[0] >= 0)
+            for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
+                gpat[sh->ti[0] * HTM_MAXACT + a] = sh->inf_pat[sh->ti[0]][a];
+        if (LEARN && sh->ti[1] >= 0)
+            for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
+                gpat[(HTM_MAXPAT + sh->ti[1]) * HTM_MAXACT + a] = sh->lrn_pat[sh->ti[1]][a];
+    } else {
+        const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
+        for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
+            const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
+            if (k < ni) {
+                const int slot = (sh->inf_head + k) % HTM_MAXPAT;
+                if (a < sh->inf_len[slot]) gpat[slot * HTM_MAXACT + a] = sh->inf_pat[slot][a];
+            } else {
+                const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
+                if (a < sh->lrn_len[slot]) gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a] = sh->lrn_pat[slot][a];
+            }
+        }
+    }
     if (threadIdx.x == 0) {
         // bitmaps out, colConfidence out (dense), pushed patterns, score
         sh->bytes += (LEARN ? 4ull : 2ull) * 4ull * c.cw + 4ull * c.ncol + (LEARN ? 4ull : 2ull) * sh->nA + 4ull;
-        hdr->stat_bytes += sh->bytes;
+        hdr->stat_bytes += sh->bytes_acc + sh->bytes;
     }
     if (threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
     if (threadIdx.x < HTM_MAXPAT) {
@@ -1850,10 +1957,10 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         sh->st_cnt[SC_HIST + hb] += 1;
     }
     if (threadIdx.x == 0 && b.dbg) {
-        uint64_t* d = b.dbg + (size_t)s * 32;
+        uint64_t* d = b.dbg + (size_t)s * 2 * HTM_NSTAMP;
         for (int k = 0; k < HTM_NSTAMP; k++) {
             d[k] += sh->st_acc[k];
-            d[16 + k] += sh->st_cnt[k];
+            d[HTM_NSTAMP + k] += sh->st_cnt[k];
         }
     }
 #endif
@@ -1887,7 +1994,8 @@ __global__ __launch_bounds__(TM_NT) HTM_RUN_ATTR void htm_run_kernel(DevCfg c, T
         if (sp_learn) sp_step_body<true>(c, sp, v, s, ssh, keep_overlaps);
         else sp_step_body<false>(c, sp, v, s, ssh, keep_overlaps);
         __syncthreads();
-        tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds);
+        tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == 0,
+                                    k == n_steps - 1);
         __syncthreads();
     }
 }

@@ -213,14 +213,14 @@ class HTMEngine:
 
     def debug_stamps(self) -> dict:
         """Per-phase TM cycle stamps + event counts (diagnostic stamps build only)."""
-        out = (ctypes.c_uint64 * 32)()
+        out = (ctypes.c_uint64 * 48)()
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
-                 "scan", "sort", "sums"]
+                 "scan", "sort", "sums", "owner", "sload", "count"]
         cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
         return dict(cycles={k: int(out[i]) for i, k in enumerate(names)},
-                    counts={k: int(out[16 + i]) for i, k in enumerate(cnames)},
-                    step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[23 + b]) for b in range(9)})
+                    counts={k: int(out[24 + i]) for i, k in enumerate(cnames)},
+                    step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[31 + b]) for b in range(9)})
 
     def frozen_index_valid(self) -> bool:
         return bool(self._L.htm_frozen_index_valid(self.h))
