@@ -225,7 +225,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // fill the LDS budget (two workgroups per CU by default).  Out-list
     // entries are window-relative u16 with 0xFFFF as padding.
     const size_t off_u = tm_step_lds_base(d, 0, 1);
-    const size_t cell_words = 4 + (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1 + FX_OWN / 2;
+    const size_t cell_words = 64 + (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1 + FX_OWN / 2;
     size_t avail = lds_budget > off_u ? (lds_budget - off_u) / 4 : 0;
     size_t win = avail > cell_words ? (avail - cell_words) * 4 : 0;
     win = (win / 1024) * 1024;

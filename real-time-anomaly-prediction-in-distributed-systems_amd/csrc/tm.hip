@@ -133,7 +133,7 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
                  (size_t)(c.q_lds + 1) / 2;
     size_t keys = learn ? 2 * (size_t)c.ncol : 0;
-    size_t col = frozen ? (size_t)c.fx_win / 4 + 4 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
+    size_t col = frozen ? (size_t)c.fx_win / 4 + 64 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
                               1 + FX_OWN / 2
                         : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
@@ -349,13 +349,14 @@ __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int t
 
 // one 16-byte block of a frozen out-list: 8 window-relative u16 slots,
 // 0xFFFF = padding; bump the slot's u8 counter
-// (padding is counted branch-free into the spare word cnt[dummy] past the counters)
+// (padding is counted branch-free into a per-lane spare word past the
+// counters, cnt[dummy + lane], so sink updates never collide)
 __device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v, uint32_t dummy) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int h = 0; h < 8; h++) {
         const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy], 1u << ((rel & 3) * 8));
+        atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy + (threadIdx.x & 63)], 1u << ((rel & 3) * 8));
     }
 }
 
@@ -530,10 +531,10 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     TmSh* sh = t.sh;
     const uint32_t W = (uint32_t)c.fx_win;
     const uint32_t mac = (uint32_t)c.max_act_cells;
-    uint32_t* cnt = t.U;  // W / 4 counter words + 4 spare (padding sink)
+    uint32_t* cnt = t.U;  // W / 4 counter words + 64 spare (padding sinks)
     const uint32_t dummy = W / 4;
-    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4 + 4);
-    uint32_t* pstart = t.U + W / 4 + 4 + (mac + 1) / 2;
+    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4 + 64);
+    uint32_t* pstart = t.U + W / 4 + 64 + (mac + 1) / 2;
     uint32_t* plo = pstart + mac + 1;
     uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
     const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
