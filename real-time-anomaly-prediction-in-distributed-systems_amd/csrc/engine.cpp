@@ -211,15 +211,18 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     {
         const size_t off_u0 = tm_step_lds_base(d, 0, 1);
         const size_t avail0 = lds_budget > off_u0 ? (lds_budget - off_u0) / 4 : 0;
-        const size_t fixed = (size_t)d.ncol + (size_t)(d.ncol + 1) / 2 + (size_t)d.ncol + 1;
+        const size_t fixed = (size_t)d.ncol + (size_t)(d.ncol + 1) / 2 + (size_t)d.ncol + 1 + (size_t)d.nw;
         size_t q = avail0 > fixed ? (avail0 - fixed) * 2 / 9 : 0;
         q = q / 64 * 64;
         if (q > 1024) q = 1024;
         if (q < 64) return fail(HTM_E_INVALID, "LDS budget %zu too small for the phase-2 buckets", lds_budget);
         d.q_lds = (int32_t)q;
     }
-    d.fin_sorted = 0;  // measured: column buckets beat the bitonic key sort at Model-1 sizes
-    if (const char* env = std::getenv("HTM_TM_FIN")) d.fin_sorted = std::strcmp(env, "sorted") == 0;
+    // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
+    // bitonic key sort at Model-1 sizes
+    d.fin_mode = 2;
+    if (const char* env = std::getenv("HTM_TM_FIN"))
+        d.fin_mode = std::strcmp(env, "sorted") == 0 ? 1 : std::strcmp(env, "buckets") == 0 ? 0 : 2;
     // frozen-inference counter window: the union region holds the u8
     // counters (fx_win bytes) plus the active-cell list and its block prefix;
     // fill the LDS budget (two workgroups per CU by default).  Out-list

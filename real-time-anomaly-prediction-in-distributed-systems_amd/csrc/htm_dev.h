@@ -57,7 +57,8 @@ struct DevCfg {
     int32_t fx_pcap;                      // frozen index: max predictive-capable segments (pid space)
     int32_t fx_noff;                      // fx_off entries per stream: ncells*fx_nwin + ncells + 1
     int32_t q_lds;                        // qualifying segments sorted in LDS (more: global path)
-    int32_t fin_sorted;                   // phase-2 tail: 1 bitonic key sort, 0 column buckets (tuning knob)
+    int32_t fin_mode;                     // phase-2 tail: 0 column buckets (scans over all columns),
+                                          // 1 bitonic key sort, 2 buckets over the nonzero-column bitmap
     int32_t max_act_cells;                // num_desired * K (frozen collection cell list)
     int32_t n_streams;
     int32_t shared_model;                 // fleet: every stream reads model instance 0 (SP + TM frozen)
@@ -249,7 +250,21 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
-// inclusive prefix sum over the wave
+// inclusive prefix sum over the wave with DPP (no LDS traffic): Hillis-
+// Steele within each 16-lane row (row_shr 1/2/4/8), then the row totals
+// carried across rows with row_bcast:15 / row_bcast:31 (gfx9 DPP).  Lanes a
+// DPP move does not reach add the `old` operand, 0.
+#ifndef HTM_SCAN_SHFL
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+#else
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     int l = lane_id();
 #pragma unroll
@@ -259,6 +274,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     }
     return v;
 }
+#endif
 
 // number of set bits of a 64-bit ballot below this lane
 __device__ __forceinline__ uint32_t ballot_rank(uint64_t ball) {

@@ -94,7 +94,7 @@ struct Tm {
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT
+    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -131,7 +131,7 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     //          block -> list map u16[FX_OWN]
     //  trim flags (learning): u32[upd_cap]
     size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
-                 (size_t)(c.q_lds + 1) / 2;
+                 (size_t)(c.q_lds + 1) / 2 + (size_t)c.nw;
     size_t keys = learn ? 2 * (size_t)c.ncol : 0;
     size_t col = frozen ? (size_t)c.fx_win / 4 + 64 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
                               1 + FX_OWN / 2
@@ -368,17 +368,27 @@ __device__ __forceinline__ void fx_collect_dense(const uint32_t* cnt, uint32_t n
     const uint32_t add = 0x01010101u * (128u - thr);
     const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
     const uint32_t n16 = nbytes / 16;
-#pragma unroll 4
-    for (uint32_t i = threadIdx.x; i < n16; i += TM_NT) {
-        const uint4 x = c4[i];
-        uint32_t m[4] = {(x.x + add) & 0x80808080u, (x.y + add) & 0x80808080u, (x.z + add) & 0x80808080u,
-                         (x.w + add) & 0x80808080u};
-        if ((m[0] | m[1] | m[2] | m[3]) == 0u) continue;
+    constexpr int U = 4;  // quads in flight per thread
+    for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += U * TM_NT) {
+        uint4 x[U];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            for (uint32_t y = m[q]; y; y &= y - 1) {
-                const uint32_t k = (uint32_t)atomicAdd(qn, 1);
-                if (k < qcap) dst[k] = base + 16 * i + 4 * q + ((__ffs(y) - 1) >> 3);
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = i0 + u * TM_NT;
+            x[u] = i < n16 ? c4[i] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = i0 + u * TM_NT;
+            uint32_t m[4] = {(x[u].x + add) & 0x80808080u, (x[u].y + add) & 0x80808080u,
+                             (x[u].z + add) & 0x80808080u, (x[u].w + add) & 0x80808080u};
+            if (i >= n16) m[0] = m[1] = m[2] = m[3] = 0u;
+            if ((m[0] | m[1] | m[2] | m[3]) == 0u) continue;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                for (uint32_t y = m[q]; y; y &= y - 1) {
+                    const uint32_t k = (uint32_t)atomicAdd(qn, 1);
+                    if (k < qcap) dst[k] = base + 16 * i + 4 * q + ((__ffs(y) - 1) >> 3);
+                }
             }
         }
     }
@@ -388,13 +398,13 @@ __device__ __forceinline__ void fx_collect_dense(const uint32_t* cnt, uint32_t n
 // only grow) appends base + slot to dst at *qn -- qualification without a
 // sweep over the counters
 __device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint32_t thr, uint32_t base, int32_t* qn,
-                                                    uint32_t* dst, uint32_t qcap) {
+                                                    uint32_t* dst, uint32_t qcap, uint32_t dummy) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t old[8];
 #pragma unroll
-    for (int h = 0; h < 8; h++) {
+    for (int h = 0; h < 8; h++) {  // branch-free: padding goes to the lane's sink word
         const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        old[h] = rel != 0xFFFFu ? atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8)) : 0u;
+        old[h] = atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy + (threadIdx.x & 63)], 1u << ((rel & 3) * 8));
     }
 #pragma unroll
     for (int h = 0; h < 8; h++) {
@@ -444,7 +454,7 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
                 STAMP_SH(shp, SB_SLOAD);
             }
 #endif
-            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap);
+            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap, dummy);
             else fx_count_block(cnt, v[j], dummy);
         }
         STAMP_SH(shp, SB_COUNT);
@@ -762,7 +772,7 @@ __device__ __forceinline__ uint32_t phase2_finish_sorted(Tm& t, uint32_t qn) {
 // NuPIC order, normalisation.  Returns numPredictedCols (uniform).
 template <bool FROZEN>
 __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
-    if (t.c.fin_sorted && (uint32_t)t.sh->qn <= (uint32_t)t.c.q_lds)
+    if (t.c.fin_mode == 1 && (uint32_t)t.sh->qn <= (uint32_t)t.c.q_lds)
         return phase2_finish_sorted<FROZEN>(t, (uint32_t)t.sh->qn);
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
@@ -779,13 +789,18 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
     uint32_t* skey = qkey + 2 * ql;
     float* sdc = reinterpret_cast<float*>(qkey + 3 * ql);
     uint16_t* qcol = reinterpret_cast<uint16_t*>(qkey + 4 * ql);
+    uint32_t* colbits = qkey + 4 * ql + (ql + 1) / 2;  // [nw] nonzero columns (fin_mode 2)
     const bool in_lds = qn <= ql;
+    const bool bitmap = c.fin_mode == 2;
     wg_clear(colcnt, c.ncol);
+    if (bitmap) wg_clear(colbits, c.nw);
     __syncthreads();
+    STAMP(t, SB_FCLR);
     // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
     uint32_t nb = phase2_pass1<FROZEN>(t, qn, [&](uint32_t k, uint32_t slot, uint32_t cell, float dc) {
         const uint32_t col = col_of(c, cell);
         atomicAdd(&colcnt[col], 1u);
+        if (bitmap) atomicOr(&colbits[col >> 5], 1u << (col & 31));
         if (in_lds) {
             qkey[k] = ((cell - col * K) << 27) | slot;
             qdc[k] = dc;
@@ -798,30 +813,68 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
     COUNT(t, SC_QN, qn);
     COUNT(t, SC_P2, 1);
     // exclusive scan of bucket counts + nonzero column list (ascending)
-    const int per = (c.ncol + TM_NT - 1) / TM_NT;
-    const int c0 = threadIdx.x * per;
-    uint32_t lsum = 0, lnz = 0;
-    for (int k = 0; k < per; k++) {
-        int col = c0 + k;
-        if (col < c.ncol && colcnt[col]) { lsum += colcnt[col]; lnz++; }
-    }
     uint32_t tsum, tnz;
-    uint32_t off = wg_excl_scan(sh, lsum, &tsum);
-    uint32_t zo = wg_excl_scan(sh, lnz, &tnz);
-    for (int k = 0; k < per; k++) {
-        int col = c0 + k;
-        if (col >= c.ncol) break;
-        uint32_t n = colcnt[col];
-        if (n) {
-            nzcol[zo] = (uint16_t)col;
-            nzstart[zo] = off;
-            zo++;
+    if (bitmap) {
+        // wave 0 walks the nonzero-column bitmap (lane l: words l, l + 64)
+        if (wave_id() == 0) {
+            const uint32_t l = lane_id();
+            uint32_t zbase = 0, obase = 0;
+            for (int r = 0; r < 2; r++) {
+                const uint32_t wi = l + 64u * r;
+                const uint32_t bits = wi < (uint32_t)c.nw ? colbits[wi] : 0u;
+                uint32_t s = 0;
+                for (uint32_t x = bits; x; x &= x - 1) s += colcnt[wi * 32 + __ffs(x) - 1];
+                const uint32_t nz = __popc(bits);
+                const uint32_t iz = wave_incl_scan(nz), is = wave_incl_scan(s);
+                uint32_t zo = zbase + iz - nz, off = obase + is - s;
+                for (uint32_t x = bits; x; x &= x - 1) {
+                    const uint32_t col = wi * 32 + __ffs(x) - 1;
+                    const uint32_t n = colcnt[col];
+                    nzcol[zo] = (uint16_t)col;
+                    nzstart[zo] = off;
+                    colcnt[col] = off;
+                    zo++;
+                    off += n;
+                }
+                zbase += __shfl(iz, 63, 64);
+                obase += __shfl(is, 63, 64);
+            }
+            if (l == 0) {
+                nzstart[zbase] = obase;
+                sh->ti[2] = (int32_t)zbase;
+                sh->ti[3] = (int32_t)obase;
+            }
         }
-        colcnt[col] = off;
-        off += n;
+        __syncthreads();
+        STAMP(t, SB_SORT);
+        tnz = (uint32_t)sh->ti[2];
+        tsum = (uint32_t)sh->ti[3];
+    } else {
+        const int per = (c.ncol + TM_NT - 1) / TM_NT;
+        const int c0 = threadIdx.x * per;
+        uint32_t lsum = 0, lnz = 0;
+        for (int k = 0; k < per; k++) {
+            int col = c0 + k;
+            if (col < c.ncol && colcnt[col]) { lsum += colcnt[col]; lnz++; }
+        }
+        uint32_t off = wg_excl_scan(sh, lsum, &tsum);
+        uint32_t zo = wg_excl_scan(sh, lnz, &tnz);
+        for (int k = 0; k < per; k++) {
+            int col = c0 + k;
+            if (col >= c.ncol) break;
+            uint32_t n = colcnt[col];
+            if (n) {
+                nzcol[zo] = (uint16_t)col;
+                nzstart[zo] = off;
+                zo++;
+            }
+            colcnt[col] = off;
+            off += n;
+        }
+        if (threadIdx.x == 0) nzstart[tnz] = tsum;
+        __syncthreads();
     }
-    if (threadIdx.x == 0) nzstart[tnz] = tsum;
-    __syncthreads();
+    (void)tsum;
     // pass 2: scatter keys (cellInColumn << 27 | slot) into column buckets
     if (in_lds) {
         for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
@@ -839,25 +892,34 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
         }
     }
     __syncthreads();
+    // pass 3a (LDS path): each entry's rank inside its column bucket (keys are
+    // unique: they hold the slot) places its dutyCycle in (cell, slot) order
+    // into qdc, dead since the scatter.  Entry-parallel with independent loads:
+    // a bucket of m entries costs m loads per entry instead of an O(m^2)
+    // dependent insertion sort on one thread.
+    if (in_lds) {
+        for (uint32_t p = threadIdx.x; p < qn; p += TM_NT) {
+            uint32_t lo = 0, hi = tnz;  // last z with nzstart[z] <= p
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (nzstart[mid] <= p) lo = mid;
+                else hi = mid;
+            }
+            const uint32_t b0 = nzstart[lo], b1 = nzstart[lo + 1];
+            const uint32_t key = skey[p];
+            uint32_t r = 0;
+            for (uint32_t j = b0; j < b1; j++) r += skey[j] < key ? 1u : 0u;
+            qdc[b0 + r] = sdc[p];
+        }
+        __syncthreads();
+    }
     // pass 3: per column, (cell, slot) order; float sum in that order
     uint32_t npcol = 0;
     for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) {
         uint32_t col = nzcol[k], lo = nzstart[k], hi = nzstart[k + 1];
         float sum = 0.0f;
         if (in_lds) {
-            for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort (buckets are small)
-                const uint32_t key = skey[i];
-                const float dc = sdc[i];
-                uint32_t j = i;
-                while (j > lo && skey[j - 1] > key) {
-                    skey[j] = skey[j - 1];
-                    sdc[j] = sdc[j - 1];
-                    j--;
-                }
-                skey[j] = key;
-                sdc[j] = dc;
-            }
-            for (uint32_t i = lo; i < hi; i++) sum += sdc[i];
+            for (uint32_t i = lo; i < hi; i++) sum += qdc[i];
         } else {
             for (uint32_t i = lo + 1; i < hi; i++) {
                 uint32_t key = t.q2[i];
@@ -874,12 +936,20 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
         if (bm_field(t.infP, col * K, K)) npcol++;
     }
     npcol = wg_sum(sh, npcol);
-    // total in nonzero-column order (ascending), sequentially as NuPIC sums it
-    if (threadIdx.x == 0) {
+    STAMP(t, SB_SUMS);
+    // total in nonzero-column order (ascending), sequentially as NuPIC sums it:
+    // wave 0 loads 64 column sums at a time and folds them lane by lane
+    // (zero padding adds +0.0f, which leaves the sum unchanged)
+    if (wave_id() == 0) {
         float tot = 0.0f;
-#pragma unroll 8
-        for (uint32_t i = 0; i < tnz; i++) tot += t.colconf[nzcol[i]];
-        sh->tf[0] = tot;
+        for (uint32_t base = 0; base < tnz; base += 64) {
+            const uint32_t i = base + lane_id();
+            const float v = i < tnz ? t.colconf[nzcol[i]] : 0.0f;
+            const int vi = __float_as_int(v);
+#pragma unroll
+            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
+        }
+        if (lane_id() == 0) sh->tf[0] = tot;
     }
     __syncthreads();
     float tot = sh->tf[0];
