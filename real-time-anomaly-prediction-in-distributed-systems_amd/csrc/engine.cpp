@@ -74,6 +74,8 @@ struct htm_engine {
     size_t ev_used = 0;
     int32_t fused = 1;              // HTM_OPT_FUSED
     int32_t run_chunk = 256;        // steps per fused htm_run launch
+    int32_t run_unit = 16;          // steps per work unit of the fused kernel's queue
+    uint32_t* wq = nullptr;         // the fused kernel's work queue: next unit + per-stream done blocks
 };
 
 extern "C" {
@@ -267,6 +269,7 @@ static int allocate(htm_engine* e) {
     const size_t S = (size_t)e->n;
     const size_t M = (size_t)e->nm;  // model instances
     const size_t cap = (size_t)d.seg_cap;
+    ALLOC(e->wq, uint32_t, S + 1);
     ALLOC(e->sp.connT, uint32_t, M * d.nin_pad * d.nw);
     ALLOC(e->sp.potmask, uint32_t, M * d.ncol * (d.nin_pad / 32));
     ALLOC(e->sp.perm, float, M * d.ncol * d.n_potential);
@@ -354,13 +357,22 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     e->nm = e->fleet ? 1 : n_streams;
     e->device = device;
     int optin = query_lds_optin();
-    size_t budget = optin >= 78 * 1024 ? (size_t)76 * 1024 : (size_t)optin - 2048;
+    // three frozen-inference workgroups per CU (HTM_RUN_WAVES): 160 KiB / 3,
+    // less the run kernel's static LDS, rounded down to 1 KiB
+    size_t budget = optin >= 54 * 1024 ? (size_t)52 * 1024 : (size_t)optin - 2048;
     if (const char* env = std::getenv("HTM_TM_LDS_BUDGET")) {  // tuning knob (bytes)
         long v = std::strtol(env, nullptr, 10);
         if (v >= 16384 && v <= optin) budget = (size_t)v;
     }
     if (const char* env = std::getenv("HTM_FUSED")) e->fused = std::atoi(env) != 0;  // A/B knob
+    if (const char* env = std::getenv("HTM_RUN_UNIT")) e->run_unit = std::max(1, std::atoi(env));  // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
+    if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
+        // shapes whose fixed LDS state leaves no room at 3 workgroups per CU
+        // (e.g. 32 cells per column) run at 2
+        budget = (size_t)76 * 1024;
+        r = derive(*cfg, n_streams, budget, e->dc);
+    }
     if (!r && e->fleet) {
         e->dc.shared_model = 1;
         e->dc.q_cap = std::min(fleet_q_cap, e->dc.seg_cap);
@@ -531,7 +543,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         HIP_TRY(hipEventRecord(ev[1], st));
     }
     if (launch_htm_run(e->dc, e->tm, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
-                       e->keep_prev, e->keep_overlaps, e->n, st))
+                       e->keep_prev, e->keep_overlaps, e->n, e->wq, e->run_unit, st))
         return fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;

@@ -2043,47 +2043,137 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
     tm_step_body<LEARN, FROZEN>(c, b, sp, scores, keep_prev, blockIdx.x, lds);
 }
 
-// Fused network.run(1) x n_steps: each workgroup steps its stream through
-// encoder -> SP -> TM -> anomaly for n_steps consecutive records, so a
-// stream never waits for the others between steps (streams are
-// independent; every stream's result is the one per-step launches give).
-// The SP's LDS aliases the TM union region, which is free between steps.
-#ifdef HTM_RUN_WAVES
-#define HTM_RUN_ATTR __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES)))
-#else
-#define HTM_RUN_ATTR
-#endif
+// Fused network.run(1) x n_steps: each work unit steps one stream through
+// encoder -> SP -> TM -> anomaly for up to unit_steps consecutive records,
+// its state LDS-resident between them (streams are independent; every
+// stream's result is the one per-step launches give).  The SP's LDS aliases
+// the TM union region, which is free between steps.
+//
+// Persistent work queue: a grid of at most (resident workgroups) dequeues
+// units u = block * n + stream in order from wq[0]; unit (s, b) waits until
+// wq[1 + s] -- stream s's completed blocks -- reaches b.  Its predecessor
+// (s, b - 1) was dequeued n units earlier by a running workgroup, so the
+// wait always ends; every workgroup exits once the counter passes the last
+// unit.  This balances streams of unequal cost (backtracks) and removes the
+// quantisation of n streams over the resident slots.  State handed between
+// units goes through HBM: agent-scope fences on both sides (the XCDs' L2s
+// are not coherent with each other).
 template <bool LEARN, bool FROZEN>
-__global__ __launch_bounds__(TM_NT) HTM_RUN_ATTR void htm_run_kernel(DevCfg c, TmBufs b, SpBufs sp, const double* values,
-                                                        float* scores, int n_steps, int sp_learn, int keep_prev,
-                                                        int keep_overlaps) {
+__device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
+                                             float* scores, int n_steps, int sp_learn, int keep_prev,
+                                             int keep_overlaps, uint32_t* wq, int unit_steps, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int s = blockIdx.x;
+    __shared__ uint32_t unit_sh[3];  // unit, its stream, its block
     SpShared& ssh = *reinterpret_cast<SpShared*>(lds + tm_layout(c, LEARN, FROZEN).off_U);
-    for (int k = 0; k < n_steps; k++) {
+    const uint32_t nblk = (uint32_t)((n_steps + unit_steps - 1) / unit_steps);
+    const uint32_t total = (uint32_t)n * nblk;
+    // one flat loop over (unit, step) so the compiler sees the same single
+    // step loop as a one-stream run (no invariants hoisted across units)
+    uint32_t u = 0xFFFFFFFFu;
+    int s = 0, k = 0, k0 = 0, k1 = 0;
+    for (;;) {
+        if (k == k1) {
+            if (u != 0xFFFFFFFFu) {
+                __threadfence();  // release this unit's state writes
+                __syncthreads();
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(&wq[1 + s], (uint32_t)(k0 / unit_steps) + 1u, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (threadIdx.x == 0) {
+                const uint32_t x = atomicAdd(&wq[0], 1u);
+                if (x < total && x >= (uint32_t)n) {
+                    const uint32_t xs = x % (uint32_t)n, blk = x / (uint32_t)n;
+                    while (__hip_atomic_load(&wq[1 + xs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < blk)
+                        __builtin_amdgcn_s_sleep(8);
+                }
+                unit_sh[0] = x;
+                unit_sh[1] = x % (uint32_t)n;
+                unit_sh[2] = x / (uint32_t)n;
+            }
+            __syncthreads();
+            // SGPR copies: the stream index must stay scalar (a VALU division
+            // result would move every per-stream address into VGPRs)
+            u = __builtin_amdgcn_readfirstlane(unit_sh[0]);
+            if (u >= total) break;
+            __threadfence();  // acquire the previous unit's state writes (all threads)
+            s = (int)__builtin_amdgcn_readfirstlane(unit_sh[1]);
+            k0 = (int)__builtin_amdgcn_readfirstlane(unit_sh[2]) * unit_steps;
+            k1 = n_steps - k0 < unit_steps ? n_steps : k0 + unit_steps;
+            k = k0;
+        }
         const double* v = values + (size_t)k * c.n_streams * c.n_fields;
         if (sp_learn) sp_step_body<true>(c, sp, v, s, ssh, keep_overlaps);
         else sp_step_body<false>(c, sp, v, s, ssh, keep_overlaps);
         __syncthreads();
-        tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == 0,
-                                    k == n_steps - 1);
+        tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
+                                    k == k1 - 1);
         __syncthreads();
+        k++;
     }
+}
+
+// The frozen-inference kernel (the bench kernel) is compiled for HTM_RUN_WAVES
+// waves per SIMD (3: three 256-thread workgroups per CU, with the LDS budget
+// sized to match); the learning kernels keep the compiler's register choice.
+#ifndef HTM_RUN_WAVES
+#define HTM_RUN_WAVES 3
+#endif
+#define HTM_RUN_ARGS                                                                                          \
+    DevCfg c, TmBufs b, SpBufs sp, const double *values, float *scores, int n_steps, int sp_learn, int keep_prev, \
+        int keep_overlaps, uint32_t *wq, int unit_steps, int n
+#define HTM_RUN_PASS c, b, sp, values, scores, n_steps, sp_learn, keep_prev, keep_overlaps, wq, unit_steps, n
+
+__global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_kernel(
+    HTM_RUN_ARGS) {
+    htm_run_body<false, true>(HTM_RUN_PASS);
+}
+template <bool LEARN>
+__global__ __launch_bounds__(TM_NT) void htm_run_kernel(HTM_RUN_ARGS) {
+    htm_run_body<LEARN, false>(HTM_RUN_PASS);
+}
+
+static int run_grid(const void* fn, size_t lds, int total) {
+    // resident workgroups: cached per (kernel, LDS size)
+    static const void* kf[8];
+    static size_t kl[8];
+    static int kg[8], nk = 0;
+    for (int i = 0; i < nk; i++)
+        if (kf[i] == fn && kl[i] == lds) return total < kg[i] ? total : kg[i];
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TM_NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    const int g = per_cu * cus;
+    if (nk < 8) {
+        kf[nk] = fn;
+        kl[nk] = lds;
+        kg[nk] = g;
+        nk++;
+    }
+    return total < g ? total : g;
 }
 
 int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
                    int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
-                   hipStream_t st) {
+                   uint32_t* wq, int unit_steps, hipStream_t st) {
+    if (n <= 0 || n_steps <= 0) return 0;
+    if (unit_steps < 1) unit_steps = 1;
     size_t lds = tm_step_lds_bytes(c, tm_learn, frozen);
+    const long nblk = (n_steps + unit_steps - 1) / unit_steps;
+    if ((long)n * nblk >= 0x7FFFFFFFL) return -1;
+    const int total = (int)(n * nblk);
+    if (hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
+    const void* fn = tm_learn ? (const void*)htm_run_kernel<true>
+                     : frozen ? (const void*)htm_run_frozen_kernel
+                              : (const void*)htm_run_kernel<false>;
+    const int grid = run_grid(fn, lds, total);
     if (tm_learn)
-        hipLaunchKernelGGL((htm_run_kernel<true, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, values, scores,
-                           n_steps, sp_learn, keep_prev, keep_overlaps);
+        hipLaunchKernelGGL((htm_run_kernel<true>), dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
     else if (frozen)
-        hipLaunchKernelGGL((htm_run_kernel<false, true>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, values, scores,
-                           n_steps, sp_learn, keep_prev, keep_overlaps);
+        hipLaunchKernelGGL(htm_run_frozen_kernel, dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
     else
-        hipLaunchKernelGGL((htm_run_kernel<false, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, values, scores,
-                           n_steps, sp_learn, keep_prev, keep_overlaps);
+        hipLaunchKernelGGL((htm_run_kernel<false>), dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2303,11 +2393,11 @@ int tm_configure_lds(const DevCfg& c) {
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
     hipError_t e2 = hipFuncSetAttribute((const void*)tm_step_kernel<false, false>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
-    hipError_t e3 = hipFuncSetAttribute((const void*)htm_run_kernel<true, false>,
+    hipError_t e3 = hipFuncSetAttribute((const void*)htm_run_kernel<true>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b0);
-    hipError_t e4 = hipFuncSetAttribute((const void*)htm_run_kernel<false, true>,
+    hipError_t e4 = hipFuncSetAttribute((const void*)htm_run_frozen_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
-    hipError_t e5 = hipFuncSetAttribute((const void*)htm_run_kernel<false, false>,
+    hipError_t e5 = hipFuncSetAttribute((const void*)htm_run_kernel<false>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
     (void)hipGetLastError();
     return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess && e4 == hipSuccess &&

@@ -6,6 +6,7 @@ for v in ${AB_VARIANTS:-"fused=1"}; do
   export HTM_FUSED=$(echo $v | sed -n 's/.*fused=\([01]\).*/\1/p')
   export HTM_TM_FIN=$(echo $v | sed -n 's/.*fin=\([a-z]*\).*/\1/p')
   b=$(echo $v | sed -n 's/.*budget=\([0-9]*\).*/\1/p'); if [ -n "$b" ]; then export HTM_TM_LDS_BUDGET=$b; else unset HTM_TM_LDS_BUDGET; fi
+  un=$(echo $v | sed -n 's/.*unit=\([0-9]*\).*/\1/p'); if [ -n "$un" ]; then export HTM_RUN_UNIT=$un; else unset HTM_RUN_UNIT; fi
   l=$(echo $v | sed -n 's/.*lib=\([a-z0-9]*\).*/\1/p'); if [ -n "$l" ]; then export HTM_AMD_LIB=libhtm_amd_$l.so; else unset HTM_AMD_LIB; fi
   tag=$(echo $v | tr ',=' '__')
   if [ "${AB_STAMPS:-1}" = "1" ]; then
