@@ -22,7 +22,9 @@
 #define TM_NT 256                  // threads of the TM workgroup (one stream)
 #endif
 #define TM_NWAVES (TM_NT / 64)
-#define FX_DEPTH 8                 // frozen index: out-list blocks in flight per thread
+#ifndef FX_DEPTH
+#define FX_DEPTH 4                 // frozen index: out-list blocks in flight per thread
+#endif
 #define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
 #define FX_MAXPER ((HTM_MAXACT * HTM_MAXK + TM_NT - 1) / TM_NT)  // active cells per thread
 #ifndef HTM_FX_PUSH

@@ -558,15 +558,20 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     const uint32_t per = (na + TM_NT - 1) / TM_NT;  // <= FX_MAXPER (na <= 64 x 32)
     const uint32_t k0 = threadIdx.x * per;
     uint32_t nblk = 0;
-    // block ranges of this thread's cells in pass w, loaded one pass ahead
-    uint32_t olo[FX_MAXPER], ohi[FX_MAXPER];
+    // block ranges of this thread's cells in pass w: the first FX_PF of them
+    // loaded one pass ahead (registers), any further ones (more than
+    // FX_PF x TM_NT active cells: K > 12) loaded in the pass
+    constexpr uint32_t FX_PF = 2;
+    uint32_t olo[FX_PF], ohi[FX_PF];
+    auto off_idx = [&](int w, uint32_t k) {
+        return w < 0 ? (size_t)c.ncells * nwin + cells[k] : (size_t)cells[k] * nwin + (uint32_t)w;
+    };
     auto load_offsets = [&](int w) {
 #pragma unroll
-        for (uint32_t j = 0; j < FX_MAXPER; j++) {
+        for (uint32_t j = 0; j < FX_PF; j++) {
             const uint32_t k = k0 + j;
             if (j < per && k < na) {
-                const size_t idx =
-                    w < 0 ? (size_t)c.ncells * nwin + cells[k] : (size_t)cells[k] * nwin + (uint32_t)w;
+                const size_t idx = off_idx(w, k);
                 olo[j] = t.fxoff[idx];
                 ohi[j] = t.fxoff[idx + 1];
             }
@@ -578,13 +583,22 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         // list of (active cell k, pass w): block range [fxoff[idx], fxoff[idx + 1])
         uint32_t lsum = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < FX_MAXPER; j++) {
+        for (uint32_t j = 0; j < FX_PF; j++) {
             const uint32_t k = k0 + j;
             if (j < per && k < na) {
                 plo[k] = olo[j];
                 pstart[k] = ohi[j] - olo[j];
                 lsum += ohi[j] - olo[j];
             }
+        }
+        for (uint32_t j = FX_PF; j < per; j++) {
+            const uint32_t k = k0 + j;
+            if (k >= na) break;
+            const size_t idx = off_idx(w, k);
+            const uint32_t lo = t.fxoff[idx], hi = t.fxoff[idx + 1];
+            plo[k] = lo;
+            pstart[k] = hi - lo;
+            lsum += hi - lo;
         }
         if (w + 1 < (int)nw) load_offsets(w + 1);
         uint32_t B;

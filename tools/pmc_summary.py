@@ -15,9 +15,13 @@ import shutil
 import statistics
 import sys
 
-src, dst, streams = sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1024
+src, dst = sys.argv[1], sys.argv[2]
+streams = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
+# steps per dispatch of the frozen kernel: the PMC passes run one htm_run chunk
+# of 256 steps (gpu_round.sh); 1 for per-step (--mode step) passes
+steps = int(sys.argv[4]) if len(sys.argv) > 4 else 256
 os.makedirs(dst, exist_ok=True)
-out = {"source": src, "streams": streams, "kernels": {}}
+out = {"source": src, "streams": streams, "steps_per_dispatch": steps, "kernels": {}}
 for name, cn in [("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")]:
     path = os.path.join(src, name, "run_counter_collection.csv")
     if not os.path.exists(path):
@@ -29,14 +33,16 @@ for name, cn in [("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")]:
     for k, v in per.items():
         e = out["kernels"].setdefault(k, {})
         e[cn] = {"dispatches": len(v), "median_kb": statistics.median(v), "mean_kb": sum(v) / len(v)}
-frozen = [k for k in out["kernels"] if "<false, true>" in k and ("htm_run_kernel" in k or "tm_step_kernel" in k)]
+frozen = [k for k in out["kernels"] if "htm_run_frozen_kernel" in k or
+          ("<false, true>" in k and ("htm_run_kernel" in k or "tm_step_kernel" in k))]
 if frozen:
     e = out["kernels"][frozen[0]]
     f = e.get("FETCH_SIZE", {}).get("median_kb", 0.0) * 1024
     w = e.get("WRITE_SIZE", {}).get("median_kb", 0.0) * 1024
     out["frozen_kernel"] = frozen[0]
-    out["per_stream_step"] = {"fetch_raw": f / streams, "fetch_corrected": 2 * f / streams, "write": w / streams,
-                              "traffic": (2 * f + w) / streams}
+    u = streams * steps
+    out["per_stream_step"] = {"fetch_raw": f / u, "fetch_corrected": 2 * f / u, "write": w / u,
+                              "traffic": (2 * f + w) / u}
 json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 ks = os.path.join(src, "prof", "run_kernel_stats.csv")
 if os.path.exists(ks):
