@@ -42,17 +42,19 @@ def make_inputs(n_total, s0, s1, t0, t1, trace):
     return np.clip(trace[(t + 97 * s) % len(trace)] + d, 0, 100).astype(np.float64)
 
 
-def trained_engine(rt, n_streams, seg_capacity, device, train_vals):
-    """Train Model 1 on one stream (2184 records, learning on), then load that
-    state into every stream of an n_streams engine."""
+def trained_engine(rt, n_streams, seg_capacity, device, train_vals, **cfg):
+    """Train Model 1 (or the config-5 cpu+mem model: cfg overrides) on one
+    stream (2184 records, learning on), then load that state into every stream
+    of an n_streams engine."""
     import torch
-    tr = rt.HTMEngine(1, device=device, seg_capacity=seg_capacity)
-    v = torch.tensor(train_vals, dtype=torch.float64, device=f"cuda:{device}").reshape(-1, 1)
+    tr = rt.HTMEngine(1, device=device, seg_capacity=seg_capacity, **cfg)
+    tv = np.asarray(train_vals, np.float64)
+    v = torch.tensor(tv.reshape(tv.shape[0], -1), device=f"cuda:{device}")
     t0 = time.time()
     tr.run(v)
     tr.status()
     train_s = time.time() - t0
-    eng = rt.HTMEngine(n_streams, device=device, seg_capacity=seg_capacity)
+    eng = rt.HTMEngine(n_streams, device=device, seg_capacity=seg_capacity, **cfg)
     for region in rt._lib.ST:
         eng.import_state(region, tr.export_state(region, 0, 1), s0=0)
     eng.replicate(0)
@@ -88,13 +90,140 @@ def cpu_baseline(trace, train_vals, n_total, target_s=12.0):
                        f"OpenMP over streams, {threads} threads), {dt:.1f} s")
 
 
+def bench_config5(args, rt, d, world, rank, local):
+    """Config 5 (BASELINE.json configs[4]): the Models 2/3 encoder -- cpu + mem
+    ScalarEncoders (ML/HTM/NetworkUtils.py:89-107, 1000 input bits) -- into a
+    4096-column SP + Model-1 TM, trained on the GPU over the reference's
+    training records (cpu, mem), replicated to every stream, learning off.
+    The timed region replays test records the ModelTesting.py way (each
+    record fed 1 + 7 times, :66-72) and, per record, runs AnomalyLikelihood on
+    the record's score (parity unpinned: NuPIC's likelihood, not in the
+    reference) and the SLO harness on the record's 8-score window
+    (ModelTesting.py:75-146, threshold 0.98, avg-response SLO 70 ms); N>1 GPUs
+    gather every record's likelihoods to rank 0 over RCCL.  `value` counts
+    network stream-steps (8 per record)."""
+    import torch
+    import torch.distributed as dist
+    W = 8
+    nf, ncol = 2, 4096
+    dev = f"cuda:{local}"
+    tr = np.stack([d["train_cpu"], d["train_mem"]], axis=1)
+    train_vals = tr[~np.isnan(tr).any(axis=1)][:2184]
+    S = args.streams
+    n_total = S * world
+    s0, s1 = rt.fleet.shard_range(n_total, world, rank)
+    eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals, n_fields=nf, sp_columns=ncol)
+    eng.set_learning(False, False)
+    n_rec = (args.warmup + args.steps) // W
+    warm_rec = args.warmup // W
+    # per-record inputs: cpu and mem test traces shifted by 97 s, each with
+    # its own PCG64(724) jitter; mean response time / violations shifted alike
+    rng = np.random.Generator(np.random.PCG64(724))
+    t_ = np.arange(n_rec)[:, None]
+    g_ = np.arange(s0, s1)[None, :]
+    idx = (t_ + 97 * g_) % len(d["test_cpu"])
+    jit = rng.integers(-2, 3, size=(2, n_rec, n_total))[:, :, s0:s1]
+    rec = np.stack([np.clip(d["test_cpu"][idx] + jit[0], 0, 100), np.clip(d["test_mem"][idx] + jit[1], 0, 100)],
+                   axis=2).astype(np.float64)  # [n_rec, S, 2]
+    rec_t = torch.tensor(rec, device=dev)
+    vals = rec_t.repeat_interleave(W, dim=0)  # [n_rec * 8, S, 2]: 1 + 7 steps per record
+    means = torch.tensor(d["test_mean"][idx].astype(np.int32), device=dev)
+    viol = torch.tensor(d["test_violations"][idx].astype(np.int32), device=dev)
+    scores = torch.empty((n_rec * W, S), dtype=torch.float32, device=dev)
+    lik = rt.harness.AnomalyLikelihood(S, device=local)
+    slo = rt.harness.SLOHarness(S, threshold=0.98, device=local)
+    liks = torch.empty((n_rec, S), dtype=torch.float64, device=dev)
+    gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
+    gathered = (torch.empty((n_rec, world, gather.width), dtype=torch.float64, device=dev)
+                if world > 1 and rank == 0 else None)
+    chunk_rec = max(1, args.chunk // W)
+
+    def replay(r0, r1, handles):
+        for a in range(r0, r1, chunk_rec):
+            b = min(r1, a + chunk_rec)
+            eng.run(vals[a * W:b * W], out=scores[a * W:b * W])
+            for r in range(a, b):
+                lik.anomaly_probability(rec_t[r], scores[r * W], out=liks[r])
+                slo.record(scores[r * W:(r + 1) * W], viol[r], means[r])
+                if gather is not None:
+                    h, _ = gather.gather(liks[r], staging=gathered[r] if rank == 0 else None)
+                    handles.append(h)
+
+    h0 = []
+    replay(0, warm_rec, h0)
+    for h in h0:
+        h.wait()
+    torch.cuda.synchronize()
+    c0 = eng.counters()
+    if not args.no_profile:
+        eng.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    handles = []
+    replay(warm_rec, n_rec, handles)
+    for h in handles:
+        h.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = eng.profile_read() if not args.no_profile else None
+    eng.profile(False)
+    c1 = eng.counters()
+    if c1["error"]:
+        raise RuntimeError(f"engine overflow flags {c1['error']}")
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    steps = (n_rec - warm_rec) * W
+    roof = None
+    if prof is not None and prof["tm_ms"] > 0:
+        tm_bytes = c1["tm_bytes"] - c0["tm_bytes"]
+        launches = prof["launches"]
+        avg_ms = prof["tm_ms"] / launches
+        achieved = tm_bytes / launches / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "traffic_source": None,
+                "kernel": "htm_run_kernel<false,true> (fused SP+TM, 4096 columns, 2 fields)",
+                "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
+                "bytes_per_launch": int(tm_bytes / launches), "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
+    st = slo.stats()
+    out = {
+        "metric": METRIC, "value": round(n_total * steps / dt, 1), "unit": "stream-steps/s", "n_gpus": world,
+        "steps": steps, "warmup": warm_rec * W, "ms_per_step": round(dt / steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f32+f64",
+        "data": "synthetic: TestingData cpu/mem traces + PCG64(724) jitter, resident in HBM (BASELINE config 5)",
+        "config": {"workload": "config5: cpu+mem encoders (1000 bits), 4096-col SP + 12-cell TM from the GPU-trained "
+                               "state, learn off; per record 1+7 steps + AnomalyLikelihood + SLO harness (0.98)",
+                   "mode": "run", "streams_per_gpu": S, "total_streams": n_total, "columns": ncol,
+                   "cells_per_column": 12, "fields": nf, "records": n_rec - warm_rec,
+                   "trained_segments": int(hdr.seg_live), "train_s": round(train_s, 2),
+                   "parallelism": f"streams sharded over {world} GPU(s)" +
+                                  (", RCCL gather of likelihoods" if world > 1 else "")},
+        "roofline": roof,
+        "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
+        "slo_totals": {k: int(v) for k, v in zip(["TP", "FP", "TN", "FN", "lead_sum"], st.sum(axis=0))},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    lik.close()
+    slo.close()
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=2,
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="2 (default, the metric's config): trained Model-1 streams, learning off; "
                          "3: fresh streams (seed 2045 + s), SP+TM learning on, 256 steps; "
-                         "4: fleet -- 131,072 streams per GPU sharing one frozen trained model")
+                         "4: fleet -- 131,072 streams per GPU sharing one frozen trained model; "
+                         "5: cpu+mem encoders, 4096-column SP, AnomalyLikelihood + SLO harness per record")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: 2324, config 3: 240)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config 2: 64, config 3: 16)")
     ap.add_argument("--streams", type=int, default=None,
@@ -111,7 +240,12 @@ def main():
     ap.add_argument("--lockstep-steps", type=int, default=256,
                     help="after the timed region, also time this many lockstep htm_step steps (0: skip)")
     args = ap.parse_args()
-    c3, c4 = args.config == 3, args.config == 4
+    c3, c4, c5 = args.config == 3, args.config == 4, args.config == 5
+    if c5:
+        args.steps = 2048 if args.steps is None else args.steps
+        args.warmup = 64 if args.warmup is None else args.warmup
+        args.streams = 1024 if args.streams is None else args.streams
+        args.seg_capacity = 128 * 1024 if args.seg_capacity is None else args.seg_capacity
     if args.steps is None:
         args.steps = 240 if c3 else 256 if c4 else 2324
     if args.warmup is None:
@@ -139,6 +273,8 @@ def main():
     rt = _pkg.load()
 
     d = np.load(os.path.join(ROOT, "tests", "golden", "model1_traces.npz"))
+    if c5:
+        return bench_config5(args, rt, d, world, rank, local)
     train_vals = [c for c, m in zip(d["train_cpu"], d["train_mem"]) if not (np.isnan(c) or np.isnan(m))][:2184]
     trace = d["test_cpu"].astype(np.float64)
 

@@ -373,6 +373,11 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
         budget = (size_t)76 * 1024;
         r = derive(*cfg, n_streams, budget, e->dc);
     }
+    if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin > 78 * 1024) {
+        // 4096 columns (config 5): one workgroup per CU
+        budget = (size_t)optin - 2048;
+        r = derive(*cfg, n_streams, budget, e->dc);
+    }
     if (!r && e->fleet) {
         e->dc.shared_model = 1;
         e->dc.q_cap = std::min(fleet_q_cap, e->dc.seg_cap);

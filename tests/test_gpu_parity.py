@@ -172,6 +172,28 @@ def test_two_field_encoder_model3_shape(rt, oracle_mod):
     tm_equal(eng, 1, orcs[1])
 
 
+def test_config5_shape_4096_columns_cpu_mem(rt, oracle_mod):
+    """BASELINE config 5 shape: cpu+mem MultiEncoder (NetworkUtils.py:89-107,
+    1000 input bits) into a 4096-column SP, Model-1 TM.  Learning on over the
+    reference's training records, then TM learning off (frozen index) on the
+    test records, the ModelTesting.py:40-44 switch."""
+    tr = np.stack([np.asarray(traces_np()["train_cpu"]), np.asarray(traces_np()["train_mem"])], axis=1)
+    tr = tr[~np.isnan(tr).any(axis=1)][:150]
+    te = np.stack([traces_np()["test_cpu"], traces_np()["test_mem"]], axis=1)[:60].astype(np.float64)
+    eng = rt.HTMEngine(1, n_fields=2, sp_columns=4096, seg_capacity=1 << 13)
+    orc = oracle_mod.OracleModel(n_fields=2, sp_columns=4096)
+    sp_equal(eng, 0, orc)
+    run_pair(eng, [orc], tr, True, True)
+    tm_equal(eng, 0, orc)
+    run_pair(eng, [orc], te, True, False)
+    sp_equal(eng, 0, orc)
+    tm_equal(eng, 0, orc)
+
+
+def traces_np():
+    return np.load(os.path.join(GOLDEN, "model1_traces.npz"))
+
+
 def test_32_cells_per_column(rt, oracle_mod):
     eng = rt.HTMEngine(1, tm_cells_per_col=32, seg_capacity=1 << 13)
     orc = oracle_mod.OracleModel(tm_cells_per_col=32)
