@@ -292,6 +292,44 @@ int htm_likelihood_destroy(htm_likelihood* lk);
 int htm_likelihood_step(htm_likelihood* lk, const double* d_values, int32_t value_stride, const float* d_scores,
                         double* d_out, void* stream);
 
+/* ---- SDRClassifier, batched over streams ---------------
+ * Replaces the "py.SDRClassifierRegion" the reference adds with alpha 0.005,
+ * steps "1,2,3,4,5,6,7" (ML/HTM/NetworkModel.py:70-97): its compute() over
+ * TM bottomUpOut + the sensor's bucketIdxOut / actValueOut (:88-95), read by
+ * getOutputData("actualValues" / "probabilities") in
+ * NetworkUtils.getPredictionResults (ML/HTM/NetworkUtils.py:166-184).
+ * NuPIC 1.0.x SDRClassifier semantics (oracle/sdr_classifier_reference.py;
+ * parity unpinned w.r.t. NuPIC).  n_inputs = TM cells (multiple of 32),
+ * n_buckets = the predicted field's bucket count (<= 1024), steps distinct,
+ * <= 16 of them.  Weights are float64 [steps][n_inputs][n_buckets] per stream. */
+typedef struct htm_classifier htm_classifier;
+int htm_cls_create(int32_t n_streams, int32_t n_inputs, int32_t n_buckets, const int32_t* steps, int32_t n_steps,
+                   double alpha, double act_value_alpha, int32_t device, htm_classifier** out);
+int htm_cls_destroy(htm_classifier* cls);
+/* One SDRClassifierRegion.compute of every stream.  d_pattern: DEVICE uint32
+ * bitmap [n_streams][n_inputs/32] (HTM_OUT_TM_OUTPUT); d_bucket DEVICE int32
+ * [n] (< 0: no learning for that stream) and d_act_value DEVICE double [n]
+ * (needed when learn); outputs (needed when infer): d_probabilities DEVICE
+ * double [n][n_steps][n_buckets] (zeros above maxBucketIdx), d_actual_values
+ * DEVICE double [n][n_buckets] (the region's actualValues output). */
+int htm_cls_compute(htm_classifier* cls, const uint32_t* d_pattern, const int32_t* d_bucket, const double* d_act_value,
+                    int32_t learn, int32_t infer, double* d_probabilities, double* d_actual_values, void* stream);
+/* Synchronise; OR of per-stream flags: 1 empty pattern, 2 bucket >= n_buckets. */
+int htm_cls_status(htm_classifier* cls, int32_t* out_flags);
+/* State regions (per stream) for save/load and tests. */
+#define HTM_CLS_ST_SCALARS 1   /* int32 [12] recordNum, maxInputIdx, maxBucketIdx, ... */
+#define HTM_CLS_ST_ACTUAL 2    /* double [n_buckets] actual-value EMA */
+#define HTM_CLS_ST_ACTUAL_OK 3 /* int32 [n_buckets] 1 where the EMA holds a value */
+#define HTM_CLS_ST_HIST_REC 4  /* int32 [max(steps)+1] history record numbers */
+#define HTM_CLS_ST_HIST_LEN 5  /* int32 [max(steps)+1] history pattern lengths */
+#define HTM_CLS_ST_HIST_IDX 6  /* uint16 [max(steps)+1][n_inputs] history patterns */
+#define HTM_CLS_ST_WEIGHTS 7   /* double [n_steps][n_inputs][n_buckets] */
+size_t htm_cls_state_bytes(const htm_classifier* cls, int32_t region);
+int htm_cls_export_state(htm_classifier* cls, int32_t region, int32_t stream_begin, int32_t n, void* h_dst,
+                         size_t bytes);
+int htm_cls_import_state(htm_classifier* cls, int32_t region, int32_t stream_begin, int32_t n, const void* h_src,
+                         size_t bytes);
+
 const char* htm_last_error(void);
 int32_t htm_abi_version(void);
 

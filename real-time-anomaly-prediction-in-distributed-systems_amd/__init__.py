@@ -6,7 +6,7 @@ is not a Python identifier); it registers this package as `rtap_amd`.
 from . import _lib
 from ._lib import HtmConfig, HtmError, build, default_config
 from .engine import HTMEngine
-from . import fleet, harness, ingest
+from . import classifier, fleet, harness, ingest
 from .harness import AnomalyLikelihood, SLOHarness
 from .network import BatchRecordStream, MultiEncoder, Network, ScalarEncoder
 

@@ -99,6 +99,8 @@ EXPORTED = [
     "htm_profile_read", "htm_counters", "htm_debug_stamps",
     "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats", "htm_create_fleet", "htm_is_fleet",
     "htm_likelihood_create", "htm_likelihood_destroy", "htm_likelihood_step",
+    "htm_cls_create", "htm_cls_destroy", "htm_cls_compute", "htm_cls_status", "htm_cls_state_bytes",
+    "htm_cls_export_state", "htm_cls_import_state",
 ]
 
 _lib = None
@@ -170,6 +172,14 @@ def lib():
     L.htm_likelihood_create.argtypes = [i32, i32, i32, i32, i32, i32, P(vp)]
     L.htm_likelihood_destroy.argtypes = [vp]
     L.htm_likelihood_step.argtypes = [vp, vp, i32, vp, vp, vp]
+    L.htm_cls_create.argtypes = [i32, i32, i32, P(i32), i32, ctypes.c_double, ctypes.c_double, i32, P(vp)]
+    L.htm_cls_destroy.argtypes = [vp]
+    L.htm_cls_compute.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, vp]
+    L.htm_cls_status.argtypes = [vp, P(i32)]
+    L.htm_cls_state_bytes.argtypes = [vp, i32]
+    L.htm_cls_state_bytes.restype = ctypes.c_size_t
+    L.htm_cls_export_state.argtypes = [vp, i32, i32, i32, vp, ctypes.c_size_t]
+    L.htm_cls_import_state.argtypes = [vp, i32, i32, i32, vp, ctypes.c_size_t]
     L.htm_slo_create.argtypes = [i32, ctypes.c_double, i32, i32, i32, P(vp)]
     L.htm_slo_destroy.argtypes = [vp]
     L.htm_slo_record.argtypes = [vp, vp, i32, vp, vp, vp, vp]

@@ -21,9 +21,12 @@ along a leading stream axis; element 0 is stream 0, so single-stream code
 that indexes `[0]` keeps working unchanged.
 
 Scope: RecordSensor (ScalarEncoder / MultiEncoder),
-SPRegion and TMRegion are executed by the engine; an SDRClassifierRegion may
-be added (NetworkModel.py:86-97 does) but is inert: its outputs raise, as the
-classifier is not on the anomaly hot path.
+SPRegion and TMRegion are executed by the engine; an SDRClassifierRegion
+(NetworkModel.py:70-97) runs on the GPU too (classifier.py, csrc/classifier.hip),
+fed TM bottomUpOut and the sensor's bucket/actual value of the first encoder
+field, its actualValues / probabilities outputs shaped like the region's
+([maxCategoryCount], [steps * maxCategoryCount]; with a leading stream axis
+when n_streams > 1).
 Errors follow the NuPIC convention of raising (NTA_THROW -> RuntimeError /
 ValueError); there is no CPU fallback -- creating the engine fails loudly if
 the HIP library or a GPU is missing.
@@ -40,6 +43,7 @@ from . import _lib
 
 SENSOR, SP, TM, CLASSIFIER = "py.RecordSensor", "py.SPRegion", "py.TMRegion", "py.SDRClassifierRegion"
 _ENGINE_FILE = "engine.htm"
+_CLS_FILE = "classifier.npz"
 _META_FILE = "network.json"
 
 
@@ -193,7 +197,14 @@ class _ClassifierImpl(_RegionImpl):
         super().__init__(params)
         steps = str(params.get("steps", "1"))
         self.stepsList = [int(x) for x in steps.split(",") if x.strip()]
-        self.maxCategoryCount = 0
+        self.maxCategoryCount = int(params.get("maxCategoryCount", 1000))  # SDRClassifierRegion default
+        self.alpha = float(params.get("alpha", 0.001))
+        if params.get("implementation", "py") not in ("py", "cpp"):
+            raise ValueError("SDRClassifier implementation %r is not supported" % params.get("implementation"))
+        self.classifier = None  # classifier.SDRClassifier, built with the engine
+        self.recordNum = 0
+        self.actualValues = None
+        self.probabilities = None
 
 
 class Region:
@@ -361,7 +372,53 @@ class Network:
             enc = m
         cfg = engine_config(enc, sp.getSelf().params, tm.getSelf().params, **self.engine_opts)
         self.engine = HTMEngine(self.n_streams, config=cfg, device=self.device)
+        self._init_classifier()
         self._learning_changed()
+
+    def _classifier_region(self):
+        rs = [r for r in self.regions.values() if r.type == CLASSIFIER]
+        if len(rs) > 1:
+            raise RuntimeError("the engine runs at most one SDRClassifierRegion per network")
+        return rs[0] if rs else None
+
+    def _init_classifier(self, cls_obj=None):
+        from .classifier import SDRClassifier
+        r = self._classifier_region()
+        if r is None:
+            return
+        impl = r.getSelf()
+        enc = self._find(SENSOR).getSelf().encoder
+        f0 = enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
+        nb = f0.n - f0.w + 1  # ScalarEncoder buckets (clipped, non-periodic)
+        if impl.maxCategoryCount < nb:
+            raise ValueError("maxCategoryCount %d < %d encoder buckets" % (impl.maxCategoryCount, nb))
+        impl.classifier = cls_obj if cls_obj is not None else SDRClassifier(
+            self.n_streams, self.engine.n_cells, nb, steps=impl.stepsList, alpha=impl.alpha,
+            device=self.engine.device)
+        impl.actualValues = np.zeros((self.n_streams, impl.maxCategoryCount))
+        impl.probabilities = np.zeros((self.n_streams, len(impl.stepsList) * impl.maxCategoryCount))
+
+    def _run_classifier(self, vals):
+        """SDRClassifierRegion.compute of every stream after the TM step: TM
+        bottomUpOut, bucketIdxOut / actValueOut of the first field (a missing
+        value does not learn)."""
+        r = self._classifier_region()
+        if r is None:
+            return
+        impl = r.getSelf()
+        learn, infer = r.modes["learningMode"], r.modes["inferenceMode"]
+        enc = self._find(SENSOR).getSelf().encoder
+        f0 = enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
+        pat = self.engine.get_output("tm_output")
+        bucket = f0.bucket_indices(vals[:, 0]) if learn else None
+        prob, act = impl.classifier.compute(pat, bucket, vals[:, 0] if learn else None, learn=learn, infer=infer)
+        impl.recordNum += 1
+        if infer:
+            nb, n = impl.classifier.n_buckets, impl.maxCategoryCount
+            impl.actualValues[:, :nb] = act.cpu().numpy()
+            p = prob.cpu().numpy()
+            for i in range(len(impl.stepsList)):
+                impl.probabilities[:, i * n:i * n + nb] = p[:, i]
 
     def _learning_changed(self):
         self._learn_dirty = True
@@ -390,6 +447,7 @@ class Network:
                                  (vals.shape, self.n_streams, self.engine.n_fields))
             sensor.values = vals
             self._scores = self.engine.step(torch.from_numpy(np.ascontiguousarray(vals).ravel()))
+            self._run_classifier(vals)
 
     def _output(self, region, name):
         if self.engine is None:
@@ -425,8 +483,18 @@ class Network:
                 a = eng.bitmap_to_dense(eng.get_output("inf_active"))
                 return a & eng.bitmap_to_dense(eng.get_output("inf_predicted"))
         elif region.type == CLASSIFIER:
-            raise NotImplementedError("SDRClassifierRegion outputs are not computed by the MI355X engine "
-                                      "(not on the anomaly path; SURVEY.md §8(f)-3)")
+            impl = region.getSelf()
+            one = (lambda a: a[0]) if self.n_streams == 1 else (lambda a: a)
+            if name == "actualValues":
+                return one(impl.actualValues.copy())
+            if name == "probabilities":
+                return one(impl.probabilities.copy())
+            if name == "categoriesOut":
+                n = impl.maxCategoryCount
+                out = np.stack([impl.actualValues[np.arange(self.n_streams),
+                                                  impl.probabilities[:, i * n:(i + 1) * n].argmax(axis=1)]
+                                for i in range(len(impl.stepsList))], axis=1)
+                return one(out)
         raise ValueError("region %s (%s) has no output %r" % (region.name, region.type, name))
 
     def scores_tensor(self):
@@ -454,6 +522,9 @@ class Network:
         with open(os.path.join(path, _META_FILE), "w") as f:
             json.dump(meta, f, indent=1)
         self.engine.save(os.path.join(path, _ENGINE_FILE))
+        cr = self._classifier_region()
+        if cr is not None:
+            cr.getSelf().classifier.save(os.path.join(path, _CLS_FILE))
         return path
 
     def _load(self, path):
@@ -478,3 +549,8 @@ class Network:
             raise RuntimeError("engine file holds %d streams, network.json says %d" %
                                (self.engine.n_streams, self.n_streams))
         self._learn_dirty = True
+        cr = self._classifier_region()
+        if cr is not None:
+            from .classifier import SDRClassifier
+            cp = os.path.join(path, _CLS_FILE)
+            self._init_classifier(SDRClassifier.load(cp, device=self.engine.device) if os.path.exists(cp) else None)

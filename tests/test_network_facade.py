@@ -116,8 +116,11 @@ def test_model1_through_the_facade_matches_golden(rt, traces, tmp_path):
             net2.run(1)
             win.append(tm2.getOutputData("anomalyScore")[0])
         assert np.array_equal(np.array(win, np.float32), g["test_windows"][r])
-    with pytest.raises(NotImplementedError):
-        net2.regions[ref.CLS].getOutputData("probabilities")
+    # the classifier (restored from the saved network) ran alongside: one
+    # distribution per step over the buckets it has seen
+    p = net2.regions[ref.CLS].getOutputData("probabilities")
+    assert p.shape == (7 * 1000,)
+    assert np.allclose(p.reshape(7, 1000).sum(axis=1), 1.0)
 
 
 @pytest.mark.gpu
