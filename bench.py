@@ -15,7 +15,7 @@ chunk without waiting for the others); the same engine is then also timed
 in lockstep (one htm_step per step, every stream waits for the slowest) and
 reported as `lockstep`.  N>1 GPUs: weak scaling, streams sharded by rank,
 RCCL gather of every step's anomaly scores to rank 0 (the SLO alerting
-path), overlapped with the next chunk.
+path) in one collective per htm_run chunk, overlapped with the next chunk.
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S]
 """
@@ -236,7 +236,10 @@ def main():
                     help="run (default): the K steps as htm_run replay chunks -- every stream steps through "
                          "the chunk without waiting for the others (the reference's offline replay of "
                          "recorded metrics, batched); step: one lockstep htm_step per step")
-    ap.add_argument("--chunk", type=int, default=256, help="steps per htm_run call in run mode")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="steps per htm_run call (= per fused launch) in run mode (config 2: all K steps; "
+                         "3, 5: 256; 4: 64)")
+    ap.add_argument("--run-unit", type=int, default=None, help="engine: steps per work-queue unit (HTM_OPT_RUN_UNIT)")
     ap.add_argument("--lockstep-steps", type=int, default=256,
                     help="after the timed region, also time this many lockstep htm_step steps (0: skip)")
     args = ap.parse_args()
@@ -254,6 +257,8 @@ def main():
         args.streams = 40960 if c3 else 131072 if c4 else 1024
     if args.seg_capacity is None:
         args.seg_capacity = 10240 if c3 else 72 * 1024
+    if args.chunk is None:
+        args.chunk = 64 if c4 else 256 if (c3 or c5) else args.steps
     if c3:
         args.lockstep_steps = 0
     if c4:
@@ -298,6 +303,10 @@ def main():
     else:
         eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals)
         eng.set_learning(False, False)
+    if not c3:
+        eng.set_run_chunk(args.chunk)  # one fused launch per htm_run call
+    if args.run_unit:
+        eng.set_run_unit(args.run_unit)
     T = args.warmup + args.steps + args.lockstep_steps
     if c4:
         # per-rank jitter stream (a 1M x T matrix per rank would not fit host memory)
@@ -312,7 +321,9 @@ def main():
     gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
     gathered = None
     if world > 1 and rank == 0:
-        gathered = torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}")
+        gathered = (torch.empty((world, args.steps, gather.width), dtype=torch.float32, device=f"cuda:{local}")
+                    if args.mode == "run" else
+                    torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}"))
 
     if args.warmup:
         eng.run(vals[:args.warmup], out=scores[:args.warmup])
@@ -330,10 +341,11 @@ def main():
             m = min(args.chunk, args.steps - c0_)
             a = args.warmup + c0_
             eng.run(vals[a:a + m], out=scores[a:a + m])
-            if world > 1:  # the chunk's scores to rank 0 (SLO alerting), overlapped with the next chunk
-                for k in range(c0_, c0_ + m):
-                    h, _ = gather.gather(scores[args.warmup + k], staging=gathered[k] if rank == 0 else None)
-                    handles.append(h)
+            if world > 1:  # the chunk's scores to rank 0 (SLO alerting) in one collective,
+                # overlapped with the next chunk
+                h, _ = gather.gather_rows(scores[a:a + m],
+                                          staging=gathered[:, c0_:c0_ + m] if rank == 0 else None)
+                handles.append(h)
     else:
         for k in range(args.steps):
             eng.step(vals[args.warmup + k], out=scores[args.warmup + k])

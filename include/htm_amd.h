@@ -121,6 +121,9 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    chunk of htm_run steps (each stream runs its chunk without
                                    waiting for the others); 0: separate SP and TM launches */
 #define HTM_OPT_RUN_CHUNK 6     /* steps per fused htm_run launch (default 256) */
+#define HTM_OPT_RUN_UNIT 7      /* steps per work-queue unit of a fused htm_run launch (0, the
+                                   default: launch steps / 8 clamped to [16, 64]); a stream's
+                                   TM state stays in LDS for a unit's steps */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Kernel times of the profiled launches since the last call (synchronises):

@@ -37,6 +37,7 @@ OPT_KEEP_OVERLAPS = 3
 OPT_PROFILE = 4
 OPT_FUSED = 5
 OPT_RUN_CHUNK = 6
+OPT_RUN_UNIT = 7
 
 
 class HtmConfig(ctypes.Structure):

@@ -74,7 +74,7 @@ struct htm_engine {
     size_t ev_used = 0;
     int32_t fused = 1;              // HTM_OPT_FUSED
     int32_t run_chunk = 256;        // steps per fused htm_run launch
-    int32_t run_unit = 16;          // steps per work unit of the fused kernel's queue
+    int32_t run_unit = 0;           // steps per work unit of the fused kernel's queue (0: auto)
     uint32_t* wq = nullptr;         // the fused kernel's work queue: next unit + per-stream done blocks
 };
 
@@ -456,6 +456,10 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         if (value < 1) return fail(HTM_E_INVALID, "run chunk must be >= 1");
         e->run_chunk = value;
     }
+    else if (opt == HTM_OPT_RUN_UNIT) {
+        if (value < 0) return fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
+        e->run_unit = value;
+    }
     else return fail(HTM_E_INVALID, "unknown option %d", opt);
     return HTM_OK;
 }
@@ -547,8 +551,13 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         HIP_TRY(hipEventRecord(ev[0], st));
         HIP_TRY(hipEventRecord(ev[1], st));
     }
+    // auto unit: a stream keeps its TM state in LDS for a unit's steps; longer
+    // units save state round trips and queue handoffs, shorter ones balance
+    // the launch's tail (measured on config 2, profiles/r01_s4/ab_unit.txt:
+    // 256-step launches best at 32, 2324-step launches flat over 48..96)
+    const int32_t unit = e->run_unit > 0 ? e->run_unit : std::max(16, std::min(64, n_steps / 8));
     if (launch_htm_run(e->dc, e->tm, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
-                       e->keep_prev, e->keep_overlaps, e->n, e->wq, e->run_unit, st))
+                       e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
         return fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;

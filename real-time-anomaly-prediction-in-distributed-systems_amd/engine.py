@@ -204,6 +204,11 @@ class HTMEngine:
         """Steps per fused htm_run launch."""
         self.set_option(_lib.OPT_RUN_CHUNK, int(steps))
 
+    def set_run_unit(self, steps: int):
+        """Steps per work-queue unit of a fused htm_run launch (a stream's TM
+        state stays in LDS across a unit)."""
+        self.set_option(_lib.OPT_RUN_UNIT, int(steps))
+
     def counters(self) -> dict:
         out = (ctypes.c_uint64 * 8)()
         check(self._L.htm_counters(self.h, out))

@@ -68,6 +68,34 @@ class ScoreGather:
         h = self.dist.gather(src.contiguous(), gather_list=gl, dst=self.dst, group=self.group, async_op=True)
         return h, staging
 
+    def gather_rows(self, block, staging=None):
+        """Start gathering a block of steps at once: this rank's `block`
+        [m, n_local] (one htm_run chunk of scores) -> rank dst's `staging`
+        [world, m, width] (allocated if None).  One collective per chunk
+        instead of one per step.  Returns (handle, staging)."""
+        import torch
+        m, n = block.shape
+        if n != self.ranges[self.rank][1] - self.ranges[self.rank][0]:
+            raise ValueError("block does not match this rank's shard")
+        src = block
+        if n != self.width:
+            src = torch.zeros((m, self.width), dtype=block.dtype, device=block.device)
+            src[:, :n] = block
+        gl = None
+        if self.rank == self.dst:
+            if staging is None:
+                staging = torch.empty((self.world, m, self.width), dtype=block.dtype, device=block.device)
+            gl = [staging[r] for r in range(self.world)]
+            if not all(t.is_contiguous() and t.shape == (m, self.width) for t in gl):
+                raise ValueError("staging must hold a contiguous [m, width] block per rank")
+        h = self.dist.gather(src.contiguous(), gather_list=gl, dst=self.dst, group=self.group, async_op=True)
+        return h, staging
+
+    def unpad_rows(self, staging):
+        """[world, m, width] padded blocks -> [m, n_total] in global stream order."""
+        import torch
+        return torch.cat([staging[r, :, : b - a] for r, (a, b) in enumerate(self.ranges)], dim=1)
+
     def unpad(self, staging):
         """[world, width] padded blocks -> [n_total] in global stream order."""
         import torch

@@ -48,8 +48,13 @@ def _worker(rank, world, port, n_total, steps, q):
         h.wait()
         if rank == 0:
             out.append(g.unpad(staging).numpy())
+    # the same scores as one block of all steps (bench.py run mode: one gather per chunk)
+    blk = torch.tensor([[((s * 7 + t) % 41) / 40.0 for s in range(a, b)] for t in range(steps)], dtype=torch.float32)
+    h, staging = g.gather_rows(blk)
+    h.wait()
     if rank == 0:
         q.put(np.stack(out))
+        q.put(g.unpad_rows(staging).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,8 +69,10 @@ def test_score_gather_two_ranks(rt, n_total):
     for p in procs:
         p.start()
     got = q.get(timeout=120)
+    got_rows = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     want = np.array([[((s * 7 + t) % 41) / 40.0 for s in range(n_total)] for t in range(steps)], np.float32)
     assert np.array_equal(got, want)
+    assert np.array_equal(got_rows, want)
