@@ -262,7 +262,7 @@ def main():
     if c3:
         args.lockstep_steps = 0
     if c4:
-        args.chunk = min(args.chunk, 64)
+        args.chunk = min(args.chunk, int(os.environ.get("HTM_C4_MAX_CHUNK", "64")))
         args.lockstep_steps = min(args.lockstep_steps, 32)
 
     import torch

@@ -2083,9 +2083,19 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
     const uint32_t total = (uint32_t)n * nblk;
     // one flat loop over (unit, step) so the compiler sees the same single
     // step loop as a one-stream run (no invariants hoisted across units)
+    // one unit per stream (n_steps <= unit_steps, e.g. every htm_step): no
+    // hand-offs, so no queue and no fences -- workgroup b runs stream b
+    const bool direct = nblk == 1;
     uint32_t u = 0xFFFFFFFFu;
     int s = 0, k = 0, k0 = 0, k1 = 0;
     for (;;) {
+        if (k == k1 && direct) {
+            if (u != 0xFFFFFFFFu || blockIdx.x >= (uint32_t)n) break;
+            u = blockIdx.x;
+            s = (int)blockIdx.x;
+            k0 = k = 0;
+            k1 = n_steps;
+        }
         if (k == k1) {
             if (u != 0xFFFFFFFFu) {
                 __threadfence();  // release this unit's state writes
@@ -2177,11 +2187,12 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     const long nblk = (n_steps + unit_steps - 1) / unit_steps;
     if ((long)n * nblk >= 0x7FFFFFFFL) return -1;
     const int total = (int)(n * nblk);
-    if (hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
+    // a single unit per stream runs on the hardware dispatcher (grid = streams)
+    if (nblk > 1 && hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
     const void* fn = tm_learn ? (const void*)htm_run_kernel<true>
                      : frozen ? (const void*)htm_run_frozen_kernel
                               : (const void*)htm_run_kernel<false>;
-    const int grid = run_grid(fn, lds, total);
+    const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
     if (tm_learn)
         hipLaunchKernelGGL((htm_run_kernel<true>), dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
     else if (frozen)
