@@ -265,3 +265,25 @@ def test_capacity_overflow_is_reported(rt):
     eng.run(vals)
     with pytest.raises(rt.HtmError):
         eng.status()
+
+
+@pytest.mark.parametrize("unit", [0, 1, 5, 64])
+def test_run_units_equal_lockstep_steps(rt, unit):
+    """htm_run through the work queue (units of `unit` steps handed between
+    workgroups; 0 = auto) equals one htm_step launch per step (the direct,
+    queue-free path), learning on then TM frozen."""
+    rng = np.random.default_rng(11)
+    vals = rng.integers(0, 101, size=(90, 5)).astype(np.float64)
+    a = rt.HTMEngine(5, seed_stride=1, seg_capacity=1 << 12)
+    b = rt.HTMEngine(5, seed_stride=1, seg_capacity=1 << 12)
+    a.set_run_unit(unit)
+    for lo, hi, tm_learn in [(0, 60, True), (60, 90, False)]:
+        a.set_learning(True, tm_learn)
+        b.set_learning(True, tm_learn)
+        ra = a.run(torch.tensor(vals[lo:hi], device="cuda")).cpu().numpy()
+        rb = np.stack([b.step(torch.tensor(vals[k], device="cuda")).cpu().numpy() for k in range(lo, hi)])
+        assert np.array_equal(ra, rb), f"unit {unit}: run and step differ in [{lo}, {hi})"
+    for s in range(5):
+        sa, sb = a.tm_states(s), b.tm_states(s)
+        for k in sa:
+            assert np.array_equal(sa[k], sb[k])
