@@ -42,17 +42,29 @@ def make_inputs(n_total, s0, s1, t0, t1, trace):
     return np.clip(trace[(t + 97 * s) % len(trace)] + d, 0, 100).astype(np.float64)
 
 
-def trained_engine(rt, n_streams, seg_capacity, device, train_vals, **cfg):
+def trained_engine(rt, n_streams, seg_capacity, device, train_vals, world=1, **cfg):
     """Train Model 1 (or the config-5 cpu+mem model: cfg overrides) on one
     stream (2184 records, learning on), then load that state into every stream
-    of an n_streams engine."""
+    of an n_streams engine.  With N>1 ranks only rank 0 trains: the trained
+    stream is broadcast to the other ranks in one collective (RCCL over xGMI,
+    fleet.broadcast_state) instead of every rank re-training it."""
     import torch
     tr = rt.HTMEngine(1, device=device, seg_capacity=seg_capacity, **cfg)
     tv = np.asarray(train_vals, np.float64)
     v = torch.tensor(tv.reshape(tv.shape[0], -1), device=f"cuda:{device}")
     t0 = time.time()
-    tr.run(v)
-    tr.status()
+    dist_info = "trained locally"
+    if world > 1:
+        import torch.distributed as dist
+        if dist.get_rank() == 0:
+            tr.run(v)
+            tr.status()
+        nb = rt.fleet.broadcast_state(tr, list(rt._lib.ST), src=0, device=f"cuda:{device}")
+        dist_info = f"trained on rank 0, broadcast to {world - 1} rank(s): {nb} B in one collective"
+    else:
+        tr.run(v)
+        tr.status()
+    torch.cuda.synchronize()
     train_s = time.time() - t0
     eng = rt.HTMEngine(n_streams, device=device, seg_capacity=seg_capacity, **cfg)
     for region in rt._lib.ST:
@@ -60,16 +72,24 @@ def trained_engine(rt, n_streams, seg_capacity, device, train_vals, **cfg):
     eng.replicate(0)
     hdr = tr.tm_header(0)
     tr.close()
-    return eng, train_s, hdr
+    return eng, train_s, hdr, dist_info
 
 
 def cpu_baseline(trace, train_vals, n_total, target_s=12.0):
-    """The C oracle (OpenMP across streams) on a bounded sample of the same
-    workload: trained Model-1 state cloned into C streams, inference only."""
+    """The C oracle (OpenMP across streams, every core this process may run
+    on) on a bounded sample of the same workload: trained Model-1 state cloned
+    into 2 x cores streams, inference only.  Beside it, the single-stream
+    Python loop over the oracle -- one network.run(1) per call, the shape of
+    ModelTesting.py:66-72's per-record loop -- and the reference's published
+    per-prediction latency."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    # every CPU this process may use: the affinity set, capped by the box's CPU
+    # allotment when it sets one (gpurun boxes export OMP_NUM_THREADS=16 per GPU
+    # while the affinity mask lists the whole host)
+    affinity = len(os.sched_getaffinity(0))
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", "0") or affinity))
     m = oracle.OracleModel()
     for v in train_vals:
         m.step(v, True, True)
@@ -85,9 +105,24 @@ def cpu_baseline(trace, train_vals, n_total, target_s=12.0):
     for k in range(1, steps + 1):
         oracle.step_batch(models, vals[k], False, False, threads)
     dt = time.time() - t0
+    # single stream, Python loop (one call per step, like ModelTesting's loop)
+    single = m.clone()
+    t0 = time.time()
+    k = 0
+    while time.time() - t0 < 4.0 and k < 4095:
+        single.step(float(vals[k + 1, 0]), False, False)
+        k += 1
+    ds = time.time() - t0
     return dict(value=n * steps / dt, unit="stream-steps/s", cores=threads, kind="port",
                 sample=f"{n} streams x {steps} steps of the config-2 workload (oracle/htm_oracle.c, "
-                       f"OpenMP over streams, {threads} threads), {dt:.1f} s")
+                       f"OpenMP over streams, {threads} threads: sched_getaffinity {affinity} capped by "
+                       f"OMP_NUM_THREADS), {dt:.1f} s",
+                single_stream_python_loop={"value": round(k / ds, 2), "unit": "stream-steps/s", "cores": 1,
+                                           "ms_per_step": round(ds / k * 1e3, 3), "steps": k,
+                                           "sample": "one stream, one oracle step per Python call "
+                                                     "(ModelTesting.py:66-72 loop shape)"},
+                reference_published={"ms_per_prediction": "20-50", "hardware": "AWS t2.large (2 vCPU), NuPIC 1.0.x",
+                                     "source": "CSC 724 Final Project Report p.8 (SURVEY.md §6)"})
 
 
 def bench_config5(args, rt, d, world, rank, local):
@@ -112,7 +147,8 @@ def bench_config5(args, rt, d, world, rank, local):
     S = args.streams
     n_total = S * world
     s0, s1 = rt.fleet.shard_range(n_total, world, rank)
-    eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals, n_fields=nf, sp_columns=ncol)
+    eng, train_s, hdr, _ = trained_engine(rt, S, args.seg_capacity, local, train_vals, world=world, n_fields=nf,
+                                          sp_columns=ncol)
     eng.set_learning(False, False)
     n_rec = (args.warmup + args.steps) // W
     warm_rec = args.warmup // W
@@ -232,16 +268,21 @@ def main():
     ap.add_argument("--seg-capacity", type=int, default=None, help="segment slots per stream")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
-    ap.add_argument("--mode", choices=["step", "run"], default="run",
-                    help="run (default): the K steps as htm_run replay chunks -- every stream steps through "
-                         "the chunk without waiting for the others (the reference's offline replay of "
-                         "recorded metrics, batched); step: one lockstep htm_step per step")
+    ap.add_argument("--mode", choices=["step", "run"], default="step",
+                    help="step (default, the headline): lockstep -- one htm_step per step, every stream "
+                         "advances one network.run(1) per step (north_star's real-time stepping); run: the K "
+                         "steps as htm_run replay chunks, each stream steps through a chunk without waiting "
+                         "for the others (the reference's offline replay of recorded metrics, batched)")
     ap.add_argument("--chunk", type=int, default=None,
                     help="steps per htm_run call (= per fused launch) in run mode (config 2: all K steps; "
                          "3, 5: 256; 4: 64)")
     ap.add_argument("--run-unit", type=int, default=None, help="engine: steps per work-queue unit (HTM_OPT_RUN_UNIT)")
-    ap.add_argument("--lockstep-steps", type=int, default=256,
-                    help="after the timed region, also time this many lockstep htm_step steps (0: skip)")
+    ap.add_argument("--other-steps", type=int, default=None,
+                    help="after the timed region, also time this many steps in the other mode (run mode "
+                         "beside the lockstep headline; config 2: 2324, config 4: 64, config 3: 0 = skip)")
+    ap.add_argument("--pmc-summary", default=None,
+                    help="JSON from tools/pmc_summary.py over rocprofv3 --pmc passes of this same command "
+                         "(same gpurun call): fills roofline.traffic; otherwise traffic is null")
     args = ap.parse_args()
     c3, c4, c5 = args.config == 3, args.config == 4, args.config == 5
     if c5:
@@ -259,11 +300,10 @@ def main():
         args.seg_capacity = 10240 if c3 else 72 * 1024
     if args.chunk is None:
         args.chunk = 64 if c4 else 256 if (c3 or c5) else args.steps
-    if c3:
-        args.lockstep_steps = 0
+    if args.other_steps is None:
+        args.other_steps = 0 if c3 else 64 if c4 else 2324
     if c4:
         args.chunk = min(args.chunk, int(os.environ.get("HTM_C4_MAX_CHUNK", "64")))
-        args.lockstep_steps = min(args.lockstep_steps, 32)
 
     import torch
     import torch.distributed as dist
@@ -293,21 +333,21 @@ def main():
         t0 = time.time()
         eng = rt.HTMEngine(S, config=cfg, device=local)
         torch.cuda.synchronize()
-        train_s, hdr = time.time() - t0, None
+        train_s, hdr, model_dist = time.time() - t0, None, "fresh per-stream init"
         eng.set_learning(True, True)
     elif c4:
         # one model trained on the GPU (2184 Model-1 records), shared by every stream
-        model, train_s, hdr = trained_engine(rt, 1, args.seg_capacity, local, train_vals)
+        model, train_s, hdr, model_dist = trained_engine(rt, 1, args.seg_capacity, local, train_vals, world=world)
         eng = rt.HTMEngine.fleet(model, S, q_capacity=4096)
         model.close()
     else:
-        eng, train_s, hdr = trained_engine(rt, S, args.seg_capacity, local, train_vals)
+        eng, train_s, hdr, model_dist = trained_engine(rt, S, args.seg_capacity, local, train_vals, world=world)
         eng.set_learning(False, False)
     if not c3:
         eng.set_run_chunk(args.chunk)  # one fused launch per htm_run call
     if args.run_unit:
         eng.set_run_unit(args.run_unit)
-    T = args.warmup + args.steps + args.lockstep_steps
+    T = args.warmup + args.steps + args.other_steps
     if c4:
         # per-rank jitter stream (a 1M x T matrix per rank would not fit host memory)
         rng = np.random.Generator(np.random.PCG64([724, s0]))
@@ -328,66 +368,29 @@ def main():
     if args.warmup:
         eng.run(vals[:args.warmup], out=scores[:args.warmup])
     torch.cuda.synchronize()
+    dev = f"cuda:{local}"
     c0 = eng.counters()
     if not args.no_profile:
         eng.profile(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    handles = []
-    if args.mode == "run":
-        for c0_ in range(0, args.steps, args.chunk):
-            m = min(args.chunk, args.steps - c0_)
-            a = args.warmup + c0_
-            eng.run(vals[a:a + m], out=scores[a:a + m])
-            if world > 1:  # the chunk's scores to rank 0 (SLO alerting) in one collective,
-                # overlapped with the next chunk
-                h, _ = gather.gather_rows(scores[a:a + m],
-                                          staging=gathered[:, c0_:c0_ + m] if rank == 0 else None)
-                handles.append(h)
-    else:
-        for k in range(args.steps):
-            eng.step(vals[args.warmup + k], out=scores[args.warmup + k])
-            if world > 1:
-                h, _ = gather.gather(scores[args.warmup + k], staging=gathered[k] if rank == 0 else None)
-                handles.append(h)
-    for h in handles:
-        h.wait()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    # the timed region: K steps bracketed by barrier + synchronize, max over ranks
+    dt, _ = timed_replay(eng, vals, scores, args.warmup, args.steps, args.mode, args.chunk, gather, gathered,
+                         rank, world, dev)
     prof = eng.profile_read() if not args.no_profile else None
     eng.profile(False)
     c1 = eng.counters()
     if c1["error"]:
         raise RuntimeError(f"engine overflow flags {c1['error']}")
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
     value = n_total * args.steps / dt
-    lockstep = None
-    if args.lockstep_steps > 0:
-        # the same engine, lockstep: one htm_step per step (per-step kernel
-        # boundary = every stream waits for the slowest one each step)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
+    other = None
+    if args.other_steps > 0:
+        # the other mode on the same engine: run mode (each stream steps through the
+        # chunk without waiting for the others) beside the lockstep headline, or back
+        omode = "run" if args.mode == "step" else "step"
         base = args.warmup + args.steps
-        for k in range(args.lockstep_steps):
-            eng.step(vals[base + k], out=scores[base + k])
-        torch.cuda.synchronize()
-        dl = time.perf_counter() - t1
-        if world > 1:
-            t = torch.tensor([dl], dtype=torch.float64, device=f"cuda:{local}")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dl = float(t.item())
-        lockstep = {"value": round(n_total * args.lockstep_steps / dl, 1), "steps": args.lockstep_steps,
-                    "ms_per_step": round(dl / args.lockstep_steps * 1e3, 4)}
+        dl, _ = timed_replay(eng, vals, scores, base, args.other_steps, omode, args.other_steps, None, None,
+                             rank, world, dev)
+        other = {"mode": omode, "value": round(n_total * args.other_steps / dl, 1), "steps": args.other_steps,
+                 "ms_per_step": round(dl / args.other_steps * 1e3, 4)}
     roof = None
     sp_bytes = 0
     if c3:
@@ -400,24 +403,23 @@ def main():
         tm_bytes = c1["tm_bytes"] - c0["tm_bytes"] + sp_bytes * S * args.steps
         launches = prof["launches"]
         avg_ms = prof["tm_ms"] / launches
-        achieved = tm_bytes / launches / (avg_ms * 1e-3) / 1e9
+        per_launch = tm_bytes / launches
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9
         traffic, tsrc = None, None
-        pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
-        if not c3 and not c4 and os.path.exists(pmc):
-            # HBM bytes per stream-step of this kernel from the committed
-            # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py)
-            ps = json.load(open(pmc)).get("per_stream_step")
-            if ps:
-                traffic = int(ps["traffic"] * S * prof["steps"] / launches)
-                tsrc = "profiles/latest_pmc.json (FETCH_SIZE x2 + WRITE_SIZE per stream-step, x streams x steps/launch)"
+        if args.pmc_summary:
+            # HBM bytes per launch measured by rocprofv3 --pmc passes of THIS command
+            # (tools/pmc_summary.py, run in the same gpurun call; corrections there)
+            pm = json.load(open(args.pmc_summary))
+            k = pm.get("kernels", {}).get(kernel_name(c3, c4, eng.fused))
+            if k:
+                traffic = int(k["hbm_bytes_per_dispatch"])
+                tsrc = f"{args.pmc_summary}: {k.get('formula', '')}"
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
-                "kernel": (("htm_run_kernel<true,false> (fused SP+TM, learning)" if c3 else
-                            "htm_run_kernel<false,true> (fused SP+TM, fleet: shared model)" if c4 else
-                            "htm_run_kernel<false,true> (fused SP+TM)") if eng.fused
-                           else "tm_step_kernel"),
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
+                "traffic_source": tsrc, "kernel": kernel_name(c3, c4, eng.fused),
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
-                "bytes_per_launch": int(tm_bytes / launches),
+                "bytes_per_launch": int(per_launch),
                 "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "stream-steps/s", "n_gpus": world,
@@ -430,15 +432,18 @@ def main():
                                 "per-stream TM state, learn off" if c4 else
                                 "config2: Model-1 streams (2048-col SP, 12-cell BacktrackingTM), SP+TM learn off, "
                                 "from the GPU-trained Model-1 state"),
-                   "mode": args.mode,
+                   "mode": ("lockstep: one htm_step (one fused launch) per step, every stream advances one "
+                            "network.run(1) per step" if args.mode == "step" else
+                            "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
                    "streams_per_gpu": S, "total_streams": n_total, "columns": 2048, "cells_per_column": 12,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
                    "segments_after": int(c1["seg_live"] // S) if c3 else None,
                    ("init_s" if c3 else "train_s"): round(train_s, 2),
+                   "model_distribution": model_dist,
                    "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL gather of scores" if world > 1 else "")},
         "roofline": roof,
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
-        "lockstep": lockstep,
+        ("run_mode" if args.mode == "step" else "lockstep"): other,
     }
     if rank == 0 and world == 1 and not args.no_cpu and not c3 and not c4:
         out["cpu_baseline"] = cpu_baseline(trace, train_vals, n_total)
@@ -447,6 +452,53 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_name(c3, c4, fused):
+    if not fused:
+        return "tm_step_kernel"
+    return ("htm_run_kernel<true> (fused SP+TM, learning)" if c3 else "htm_run_frozen_kernel (fused SP+TM, frozen TM)")
+
+
+def timed_replay(eng, vals, scores, a, steps, mode, chunk, gather, gathered, rank, world, device):
+    """Steps [a, a + steps) of every stream, timed between barrier +
+    synchronize on both sides, the max over ranks returned (the bench
+    contract).  mode "step": one eng.step per step (lockstep) and, with N>1
+    ranks, each step's scores gathered to rank 0 (SLO alerting input);
+    "run": eng.run chunks of `chunk` steps, one gather_rows per chunk,
+    overlapped with the next chunk.  Returns (seconds, gathered)."""
+    import torch
+    import torch.distributed as dist
+    import _pkg
+    max_over_ranks = _pkg.load().fleet.max_over_ranks
+    cuda = torch.cuda.is_available() and str(device).startswith("cuda")
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    handles = []
+    if mode == "run":
+        for c0_ in range(0, steps, chunk):
+            m = min(chunk, steps - c0_)
+            eng.run(vals[a + c0_:a + c0_ + m], out=scores[a + c0_:a + c0_ + m])
+            if gather is not None:
+                h, _ = gather.gather_rows(scores[a + c0_:a + c0_ + m],
+                                          staging=gathered[:, c0_:c0_ + m] if rank == 0 else None)
+                handles.append(h)
+    else:
+        for k in range(steps):
+            eng.step(vals[a + k], out=scores[a + k])
+            if gather is not None:
+                h, _ = gather.gather(scores[a + k], staging=gathered[k] if rank == 0 else None)
+                handles.append(h)
+    for h in handles:
+        h.wait()
+    sync()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    return max_over_ranks(dt, device if cuda else None), gathered
 
 
 if __name__ == "__main__":

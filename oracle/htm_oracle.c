@@ -205,7 +205,11 @@ static void sp_update_perm_for_column(const orc_params* p, sp_t* sp, float* perm
 
 static float sp_init_perm_connected(const orc_params* p, sp_t* sp) {
     float span = sp->perm_max - p->sp_perm_connected;
-    float q = p->sp_perm_connected + (float)((double)span * rng_real64(&sp->rng));
+    float q;
+    if (p->variant & ORC_VAR_SP_INIT_DOUBLE)
+        q = (float)((double)p->sp_perm_connected + (double)span * rng_real64(&sp->rng));
+    else
+        q = p->sp_perm_connected + (float)((double)span * rng_real64(&sp->rng));
     q = (float)((double)(int32_t)(q * 100000.0f) / 100000.0);
     return q;
 }
@@ -254,7 +258,8 @@ static void sp_init(const orc_params* p, sp_t* sp) {
 
     /* potentialRadius = inputWidth (SPRegion), capped at numInputs */
     uint32_t radius = (uint32_t)nin;
-    for (int c = 0; c < ncol; c++) sp->tie_breaker[c] = (float)(0.01 * rng_real64(&sp->rng));
+    for (int c = 0; c < ncol; c++)
+        sp->tie_breaker[c] = (p->variant & ORC_VAR_SP_NO_TIEBREAKER) ? 0.0f : (float)(0.01 * rng_real64(&sp->rng));
 
     uint32_t* pop = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)nin);
     uint32_t* sel = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)nin);
@@ -270,6 +275,7 @@ static void sp_init(const orc_params* p, sp_t* sp) {
         for (uint32_t k = 0; k < count; k++) {
             int32_t coordk = (center - (int32_t)radius + (int32_t)k) % nin;
             if (coordk < 0) coordk += nin;
+            if (p->variant & ORC_VAR_SP_POOL_ASCEND) coordk = (int32_t)k;
             pop[k] = (uint32_t)coordk;
         }
         uint32_t numPotential = (uint32_t)roundf((float)count * p->sp_potential_pct);
@@ -325,9 +331,11 @@ static int sp_inhibit_global(const orc_params* p, const sp_t* sp, const float* o
     int n = 0;
     for (int i = 0; i < sp->ncol; i++) {
         if (ov[i] < (float)p->sp_stimulus_threshold) continue;
-        if ((uint32_t)n < numDesired || ov[i] >= ov[winners[n - 1]]) {
+        int low = (p->variant & ORC_VAR_SP_TIE_LOW) != 0;
+        if ((uint32_t)n < numDesired || ov[i] > ov[winners[n - 1]] || (!low && ov[i] == ov[winners[n - 1]])) {
             int pos = 0;
-            while (pos < n && !(ov[i] >= ov[winners[pos]])) pos++;
+            if (low) while (pos < n && !(ov[i] > ov[winners[pos]])) pos++;
+            else while (pos < n && !(ov[i] >= ov[winners[pos]])) pos++;
             memmove(winners + pos + 1, winners + pos, sizeof(int32_t) * (size_t)(n - pos));
             winners[pos] = i;
             n++;
@@ -466,6 +474,7 @@ typedef struct {
     uint32_t* cand;   /* scratch: candidate cells */
     uint32_t* cand2;
     int64_t stats[4]; /* inferPhase2 calls, inferBacktracks, lrnPhase2 calls, lrnBacktracks */
+    uint32_t variant;
 } tm_t;
 
 static const uint32_t DC_TIERS[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 100000, 320000};
@@ -591,6 +600,7 @@ static void tm_init(const orc_params* p, tm_t* tm) {
     for (int k = 0; k < p->tm_max_lrn_backtrack + 2; k++)
         tm->lrn_pat[k].cols = (int32_t*)calloc((size_t)tm->ncol, 4);
     tm->pam_counter = p->tm_pam_length;
+    tm->variant = p->variant;
     tm->colmask = (uint8_t*)calloc((size_t)tm->ncol, 1);
     tm->cand = (uint32_t*)calloc(nc, 4);
     tm->cand2 = (uint32_t*)calloc(nc, 4);
@@ -678,6 +688,7 @@ static void tm_copy(const orc_params* p, tm_t* d, const tm_t* s) {
     free(to);
     d->lrn_iter = s->lrn_iter;
     d->iter = s->iter;
+    d->variant = s->variant;
     d->pam_counter = s->pam_counter;
     d->learned_seq_length = s->learned_seq_length;
     d->reset_called = s->reset_called;
@@ -810,6 +821,19 @@ static void tm_get_segment_active_synapses(const orc_params* p, tm_t* tm, int c,
 static int tm_best_matching_cell(tm_t* tm, int c, const uint8_t* state, int min_threshold,
                                  seg_t** best_seg, int* best_act) {
     int bestActivityInCol = min_threshold, bestSegIdxInCol = -1, bestCellInCol = -1;
+    if (tm->variant & ORC_VAR_TM_BMC_SEG_GE) {
+        for (int i = 0; i < tm->K; i++) {
+            cell_t* cl = &tm->cells[c * tm->K + i];
+            for (int j = 0; j < cl->n; j++) {
+                int a = seg_activity(cl->s[j], state);
+                if (a >= bestActivityInCol) { bestActivityInCol = a; bestSegIdxInCol = j; bestCellInCol = i; }
+            }
+        }
+        if (bestCellInCol == -1) { *best_seg = NULL; *best_act = 0; return -1; }
+        *best_seg = tm->cells[c * tm->K + bestCellInCol].s[bestSegIdxInCol];
+        *best_act = bestActivityInCol;
+        return bestCellInCol;
+    }
     for (int i = 0; i < tm->K; i++) {
         cell_t* cl = &tm->cells[c * tm->K + i];
         int maxSegActivity = 0, maxSegIdx = 0;
@@ -868,21 +892,30 @@ static int cmp_perm_idx(const void* a, const void* b) {
     return (x[1] > y[1]) - (x[1] < y[1]);
 }
 
+static int cmp_perm_idx_late(const void* a, const void* b) {
+    const float* x = (const float*)a;
+    const float* y = (const float*)b;
+    if (x[0] < y[0]) return -1;
+    if (x[0] > y[0]) return 1;
+    return (x[1] < y[1]) - (x[1] > y[1]);
+}
+
 /* Segment.freeNSynapses(numToFree, inactiveSynapseIndices) */
-static void seg_free_n_synapses(seg_t* s, int num_to_free, const uint8_t* inactive) {
+static void seg_free_n_synapses(seg_t* s, int num_to_free, const uint8_t* inactive, int late) {
+    int (*cmp)(const void*, const void*) = late ? cmp_perm_idx_late : cmp_perm_idx;
     float keys[2 * ORC_MAXSYN * 2];
     int cands[ORC_MAXSYN * 2], ncand = 0;
     /* lowest-permanence inactive synapses first (stable by index) */
     int ni = 0;
     for (int k = 0; k < s->nsyn; k++)
         if (inactive[k]) { keys[2 * ni] = s->syn[k].perm; keys[2 * ni + 1] = (float)k; ni++; }
-    qsort(keys, (size_t)ni, 2 * sizeof(float), cmp_perm_idx);
+    qsort(keys, (size_t)ni, 2 * sizeof(float), cmp);
     for (int k = 0; k < ni && ncand < num_to_free; k++) cands[ncand++] = (int)keys[2 * k + 1];
     if (ncand < num_to_free) {
         int na = 0;
         for (int k = 0; k < s->nsyn; k++)
             if (!inactive[k]) { keys[2 * na] = s->syn[k].perm; keys[2 * na + 1] = (float)k; na++; }
-        qsort(keys, (size_t)na, 2 * sizeof(float), cmp_perm_idx);
+        qsort(keys, (size_t)na, 2 * sizeof(float), cmp);
         for (int k = 0; k < na && ncand < num_to_free; k++) cands[ncand++] = (int)keys[2 * k + 1];
     }
     uint8_t del[ORC_MAXSYN * 2];
@@ -922,7 +955,7 @@ static int tm_adapt_segment(const orc_params* p, tm_t* tm, const segupd_t* u) {
         }
         if (p->tm_max_syn_per_seg > 0 && u->n_new + s->nsyn > p->tm_max_syn_per_seg) {
             int num_to_free = s->nsyn + u->n_new - p->tm_max_syn_per_seg;
-            seg_free_n_synapses(s, num_to_free, inactive);
+            seg_free_n_synapses(s, num_to_free, inactive, (tm->variant & ORC_VAR_TM_FREE_LATE) != 0);
         }
         for (int k = 0; k < u->n_new; k++) seg_add_syn(s, u->newsrc[k], p->tm_initial_perm);
     } else {
@@ -1160,7 +1193,7 @@ static int tm_infer_phase2(const orc_params* p, tm_t* tm) {
                 seg_t* s = cl->s[j];
                 int nact = seg_activity(s, tm->infA_t);
                 if (nact < p->tm_activation_threshold) continue;
-                float dc = seg_duty_cycle(s, tm->lrn_iter, 0, 0);
+                float dc = seg_duty_cycle(s, tm->lrn_iter, 0, (tm->variant & ORC_VAR_TM_DC_READONLY) != 0);
                 tm->cellConf_t[c * K + i] += dc;
                 tm->colConf_t[c] += dc;
                 if (seg_is_active(p, s, tm->infA_t)) tm->infP_t[c * K + i] = 1;
@@ -1211,7 +1244,7 @@ static void tm_infer_backtrack(const orc_params* p, tm_t* tm) {
         memcpy(tm->infP_cand, tm->infP_t, nc);
         memcpy(tm->cellConf_cand, tm->cellConf_t, nc * 4);
         memcpy(tm->colConf_cand, tm->colConf_t, (size_t)tm->ncol * 4);
-        break;
+        if (!(tm->variant & ORC_VAR_TM_BT_LAST_START)) break;
     }
     if (!haveCand) {
         memcpy(tm->infA_t, tm->infA_backup, nc);
@@ -1250,6 +1283,13 @@ static void tm_update_inference_state(const orc_params* p, tm_t* tm, const int32
 static void tm_compute(const orc_params* p, tm_t* tm, const int32_t* active, int nA, int learn) {
     if (learn) tm->lrn_iter++;
     tm->iter++;
+    if (learn && (tm->variant & ORC_VAR_TM_DC_TIERS)) {
+        int tier = 0;
+        for (int t = 1; t < 9; t++) tier |= tm->lrn_iter == DC_TIERS[t];
+        if (tier)
+            for (int c = 0; c < tm->ncells; c++)
+                for (int j = 0; j < tm->cells[c].n; j++) (void)seg_duty_cycle(tm->cells[c].s[j], tm->lrn_iter, 0, 0);
+    }
     if (!tm->have_avg_density) {
         tm->avg_input_density = (double)nA;
         tm->have_avg_density = 1;

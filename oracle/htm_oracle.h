@@ -65,7 +65,21 @@ typedef struct {
     int32_t tm_max_seq_length; /* 32 */
     int32_t tm_seg_update_valid_duration; /* 5 */
     uint64_t tm_seed;          /* 2045 */
+    /* Alternatives for the Appendix A [L]/[M] choices (ORC_VAR_* bits; 0 = the
+     * frozen restatement the HIP engine is held bit-exact to).  Only used by
+     * oracle/variant_sweep.py to A/B them against ML/Data/result_model1.txt. */
+    uint32_t variant;
 } orc_params;
+
+#define ORC_VAR_SP_TIE_LOW       0x001u /* global inhibition: ties -> LOWER index (strict '>' admission) */
+#define ORC_VAR_SP_NO_TIEBREAKER 0x002u /* SP init draws no 2048-entry tieBreaker before the pools */
+#define ORC_VAR_SP_INIT_DOUBLE   0x004u /* initPermConnected_: 0.1f + span*u summed in double (C++ promotion) */
+#define ORC_VAR_SP_POOL_ASCEND   0x008u /* potential-pool population in ascending input order (no wrap centre) */
+#define ORC_VAR_TM_BMC_SEG_GE    0x010u /* getBestMatchingCell: last segment with '>=' over the column (Cells4 form) */
+#define ORC_VAR_TM_DC_TIERS      0x020u /* refresh every segment's duty cycle when lrnIter crosses a tier */
+#define ORC_VAR_TM_DC_READONLY   0x040u /* inferPhase2 reads segment duty cycles read-only */
+#define ORC_VAR_TM_FREE_LATE     0x080u /* freeNSynapses: equal-permanence ties free the LATER synapse first */
+#define ORC_VAR_TM_BT_LAST_START 0x100u /* inferBacktrack: prefer the in-sequence start CLOSEST to now */
 
 typedef struct orc_model orc_model;
 

@@ -36,6 +36,7 @@ class OrcParams(ctypes.Structure):
         ("tm_pam_length", ctypes.c_int32), ("tm_max_inf_backtrack", ctypes.c_int32),
         ("tm_max_lrn_backtrack", ctypes.c_int32), ("tm_max_seq_length", ctypes.c_int32),
         ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
+        ("variant", ctypes.c_uint32),
     ]
 
 

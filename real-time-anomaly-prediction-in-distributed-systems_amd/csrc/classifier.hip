@@ -44,7 +44,8 @@ struct ClsState {
     int32_t infer_buckets;  // maxBucketIdx + 1 seen by this record's inference
     int32_t hist_n, hist_head;
     int32_t cur_rec, cur_slot;  // this record's number and history slot
-    int32_t err;            // 1: empty pattern (NuPIC max() of an empty list), 2: bucket >= nbuckets
+    int32_t err;            // 1: THIS record's pattern is empty (NuPIC max() of an empty list; the record
+                            //    is skipped, later records run), 2: bucket >= nbuckets (sticky)
     int32_t learn_bucket;   // this record's bucket (-1: no learning)
     int32_t pad[2];
 };
@@ -197,6 +198,7 @@ __global__ void __launch_bounds__(CLS_NT) cls_prep_kernel(ClsBufs c, const uint3
         st->record_num = rec + 1;
         st->infer_buckets = old_b + 1;
         st->learn_bucket = -1;
+        st->err &= ~1;  // per-record flag: an empty pattern skips only this record
         if (total == 0) {
             st->err |= 1;
         } else {
@@ -280,16 +282,16 @@ int htm_cls_create(int32_t n_streams, int32_t n_inputs, int32_t n_buckets, const
                    double alpha, double act_value_alpha, int32_t device, htm_classifier** out) {
     if (!out || !steps || n_streams < 1 || n_inputs < 32 || n_inputs % 32 || n_inputs > 65536 || n_buckets < 1 ||
         n_buckets > CLS_NB_MAX || n_steps < 1 || n_steps > CLS_MAX_STEPS)
-        return HTM_E_INVALID;
+        return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     int mx = 0;
     for (int i = 0; i < n_steps; i++) {
-        if (steps[i] < 0 || steps[i] > 1000) return HTM_E_INVALID;
+        if (steps[i] < 0 || steps[i] > 1000) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
         for (int j = 0; j < i; j++)
-            if (steps[j] == steps[i]) return HTM_E_INVALID;
+            if (steps[j] == steps[i]) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
         mx = steps[i] > mx ? steps[i] : mx;
     }
     *out = nullptr;
-    if (hipSetDevice(device) != hipSuccess) return HTM_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     htm_classifier* h = new htm_classifier();
     h->device = device;
     ClsBufs& b = h->b;
@@ -316,7 +318,7 @@ int htm_cls_create(int32_t n_streams, int32_t n_inputs, int32_t n_buckets, const
         if (hipMalloc(a.p, a.bytes) != hipSuccess || hipMemset(*a.p, 0, a.bytes) != hipSuccess) {
             (void)hipGetLastError();
             htm_cls_destroy(h);
-            return HTM_E_HIP;
+            return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
         }
     }
     *out = h;
@@ -326,13 +328,13 @@ int htm_cls_create(int32_t n_streams, int32_t n_inputs, int32_t n_buckets, const
 int htm_cls_compute(htm_classifier* h, const uint32_t* d_pattern, const int32_t* d_bucket, const double* d_act_value,
                     int32_t learn, int32_t infer, double* d_probabilities, double* d_actual_values, void* stream) {
     if (!h || !d_pattern || (learn && (!d_bucket || !d_act_value)) || (infer && (!d_probabilities || !d_actual_values)))
-        return HTM_E_INVALID;
+        return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(cls_prep_kernel, dim3(h->b.n), dim3(CLS_NT), 0, st, h->b, d_pattern, d_bucket, d_act_value,
                        learn ? 1 : 0, infer ? 1 : 0, d_actual_values);
     hipLaunchKernelGGL(cls_step_kernel, dim3(h->b.n, h->b.nsteps), dim3(CLS_NT), 0, st, h->b, infer ? 1 : 0,
                        d_probabilities);
-    return hipGetLastError() == hipSuccess ? HTM_OK : HTM_E_HIP;
+    return hipGetLastError() == hipSuccess ? HTM_OK : htm_fail(HTM_E_HIP, "%s: HIP launch/sync failed", __func__);
 }
 
 static int cls_region(const htm_classifier* h, int32_t region, void** base, size_t* per) {
@@ -345,7 +347,7 @@ static int cls_region(const htm_classifier* h, int32_t region, void** base, size
         case HTM_CLS_ST_HIST_LEN: *base = b.hlen; *per = (size_t)b.H * 4; return HTM_OK;
         case HTM_CLS_ST_HIST_IDX: *base = b.hidx; *per = (size_t)b.H * b.ncells * 2; return HTM_OK;
         case HTM_CLS_ST_WEIGHTS: *base = b.w; *per = (size_t)b.nsteps * b.ncells * b.nb * 8; return HTM_OK;
-        default: return HTM_E_INVALID;
+        default: return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     }
 }
 
@@ -359,13 +361,13 @@ size_t htm_cls_state_bytes(const htm_classifier* h, int32_t region) {
 static int cls_copy(htm_classifier* h, int32_t region, int32_t s0, int32_t n, void* host, size_t bytes, int to_dev) {
     void* base;
     size_t per;
-    if (!h || !host || s0 < 0 || n < 1 || s0 + n > h->b.n || cls_region(h, region, &base, &per)) return HTM_E_INVALID;
-    if (bytes != per * n) return HTM_E_INVALID;
-    if (hipSetDevice(h->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return HTM_E_HIP;
+    if (!h || !host || s0 < 0 || n < 1 || s0 + n > h->b.n || cls_region(h, region, &base, &per)) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
+    if (bytes != per * n) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
+    if (hipSetDevice(h->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     char* d = (char*)base + per * s0;
     hipError_t e = to_dev ? hipMemcpy(d, host, bytes, hipMemcpyHostToDevice)
                           : hipMemcpy(host, d, bytes, hipMemcpyDeviceToHost);
-    return e == hipSuccess ? HTM_OK : HTM_E_HIP;
+    return e == hipSuccess ? HTM_OK : htm_fail(HTM_E_HIP, "%s: HIP launch/sync failed", __func__);
 }
 
 int htm_cls_export_state(htm_classifier* h, int32_t region, int32_t s0, int32_t n, void* h_dst, size_t bytes) {
@@ -377,14 +379,14 @@ int htm_cls_import_state(htm_classifier* h, int32_t region, int32_t s0, int32_t 
 }
 
 int htm_cls_status(htm_classifier* h, int32_t* out_flags) {
-    if (!h || !out_flags) return HTM_E_INVALID;
-    if (hipSetDevice(h->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return HTM_E_HIP;
+    if (!h || !out_flags) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
+    if (hipSetDevice(h->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     ClsState* hs = new ClsState[h->b.n];
     const hipError_t e = hipMemcpy(hs, h->b.st, sizeof(ClsState) * h->b.n, hipMemcpyDeviceToHost);
     int32_t f = 0;
     for (int s = 0; s < h->b.n; s++) f |= hs[s].err;
     delete[] hs;
-    if (e != hipSuccess) return HTM_E_HIP;
+    if (e != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     *out_flags = f;
     return HTM_OK;
 }

@@ -19,11 +19,11 @@
 
 #include "htm_dev.h"
 
-namespace {
+static thread_local std::string g_err;
 
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) {
+// the message htm_last_error() returns; every HTM_E_* return of the library
+// goes through here (engine.cpp and the slo / likelihood / classifier units)
+int htm_fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -33,10 +33,12 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+namespace {
+
 #define HIP_TRY(x)                                                                          \
     do {                                                                                    \
         hipError_t e_ = (x);                                                                \
-        if (e_ != hipSuccess) return fail(HTM_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
     } while (0)
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -125,30 +127,30 @@ void htm_default_config(htm_config* c) {
 }  // extern "C"
 
 static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) {
-    if (c.n_fields < 1 || c.n_fields > 4) return fail(HTM_E_INVALID, "n_fields must be 1..4");
+    if (c.n_fields < 1 || c.n_fields > 4) return htm_fail(HTM_E_INVALID, "n_fields must be 1..4");
     if (c.enc_w < 1 || c.enc_w >= c.enc_n || c.enc_n * c.n_fields > 2048)
-        return fail(HTM_E_INVALID, "encoder n/w out of range");
-    if (c.n_fields * c.enc_w >= 128) return fail(HTM_E_INVALID, "n_fields*w must be < 128");
+        return htm_fail(HTM_E_INVALID, "encoder n/w out of range");
+    if (c.n_fields * c.enc_w >= 128) return htm_fail(HTM_E_INVALID, "n_fields*w must be < 128");
     if (c.sp_columns < 64 || c.sp_columns % 64 != 0 || c.sp_columns > 4096)
-        return fail(HTM_E_INVALID, "sp_columns must be a multiple of 64 in [64, 4096]");
-    if (c.sp_num_active < 1 || c.sp_num_active > HTM_MAXACT) return fail(HTM_E_INVALID, "sp_num_active must be 1..64");
-    if (c.sp_boost_strength != 0.0f) return fail(HTM_E_INVALID, "only boostStrength 0 is supported");
-    if (c.sp_stimulus_threshold < 0 || c.sp_stimulus_threshold > 127) return fail(HTM_E_INVALID, "stimulus threshold");
-    if (c.tm_cells_per_col < 2 || c.tm_cells_per_col > HTM_MAXK) return fail(HTM_E_INVALID, "cells_per_col must be 2..32");
-    if ((int64_t)c.sp_columns * c.tm_cells_per_col > 65536) return fail(HTM_E_INVALID, "columns*cells must be <= 65536");
-    if (c.tm_max_syn_per_seg < 1 || c.tm_max_syn_per_seg > HTM_MAXSYN) return fail(HTM_E_INVALID, "max_syn_per_seg 1..32");
+        return htm_fail(HTM_E_INVALID, "sp_columns must be a multiple of 64 in [64, 4096]");
+    if (c.sp_num_active < 1 || c.sp_num_active > HTM_MAXACT) return htm_fail(HTM_E_INVALID, "sp_num_active must be 1..64");
+    if (c.sp_boost_strength != 0.0f) return htm_fail(HTM_E_INVALID, "only boostStrength 0 is supported");
+    if (c.sp_stimulus_threshold < 0 || c.sp_stimulus_threshold > 127) return htm_fail(HTM_E_INVALID, "stimulus threshold");
+    if (c.tm_cells_per_col < 2 || c.tm_cells_per_col > HTM_MAXK) return htm_fail(HTM_E_INVALID, "cells_per_col must be 2..32");
+    if ((int64_t)c.sp_columns * c.tm_cells_per_col > 65536) return htm_fail(HTM_E_INVALID, "columns*cells must be <= 65536");
+    if (c.tm_max_syn_per_seg < 1 || c.tm_max_syn_per_seg > HTM_MAXSYN) return htm_fail(HTM_E_INVALID, "max_syn_per_seg 1..32");
     if (c.tm_new_syn_count < 1 || c.tm_new_syn_count > c.tm_max_syn_per_seg)
-        return fail(HTM_E_INVALID, "new_syn_count must be 1..max_syn_per_seg");
-    if (c.tm_max_segs_per_cell < 1 || c.tm_max_segs_per_cell > 255) return fail(HTM_E_INVALID, "max_segs_per_cell 1..255");
+        return htm_fail(HTM_E_INVALID, "new_syn_count must be 1..max_syn_per_seg");
+    if (c.tm_max_segs_per_cell < 1 || c.tm_max_segs_per_cell > 255) return htm_fail(HTM_E_INVALID, "max_segs_per_cell 1..255");
     if (c.tm_max_inf_backtrack < 0 || c.tm_max_inf_backtrack > HTM_MAXPAT - 1 || c.tm_max_lrn_backtrack < 0 ||
         c.tm_max_lrn_backtrack > HTM_MAXPAT - 1)
-        return fail(HTM_E_INVALID, "backtrack depth must be 0..15");
-    if (c.tm_pam_length < 1) return fail(HTM_E_INVALID, "pamLength must be > 0");
+        return htm_fail(HTM_E_INVALID, "backtrack depth must be 0..15");
+    if (c.tm_pam_length < 1) return htm_fail(HTM_E_INVALID, "pamLength must be > 0");
     if (c.tm_activation_threshold < 1 || c.tm_activation_threshold > HTM_MAXSYN || c.tm_min_threshold < 1 ||
         c.tm_min_threshold > HTM_MAXSYN)
-        return fail(HTM_E_INVALID, "activation/min thresholds must be 1..32");
-    if (c.seg_capacity < 64 || c.seg_capacity > (1 << 27)) return fail(HTM_E_INVALID, "seg_capacity");
-    if (c.upd_capacity < 1 || c.upd_capacity > 65535) return fail(HTM_E_INVALID, "upd_capacity");
+        return htm_fail(HTM_E_INVALID, "activation/min thresholds must be 1..32");
+    if (c.seg_capacity < 64 || c.seg_capacity > (1 << 27)) return htm_fail(HTM_E_INVALID, "seg_capacity");
+    if (c.upd_capacity < 1 || c.upd_capacity > 65535) return htm_fail(HTM_E_INVALID, "upd_capacity");
     std::memset(&d, 0, sizeof(d));
     d.n_fields = c.n_fields;
     d.enc_n = c.enc_n;
@@ -170,7 +172,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     float density = (float)c.sp_num_active / (float)area;
     if (density > 0.5f) density = 0.5f;
     d.num_desired = (int32_t)(uint32_t)(density * (float)c.sp_columns);
-    if (d.num_desired > HTM_MAXACT) return fail(HTM_E_INVALID, "too many winners");
+    if (d.num_desired > HTM_MAXACT) return htm_fail(HTM_E_INVALID, "too many winners");
     d.stim_thr = c.sp_stimulus_threshold;
     d.dc_period = c.sp_duty_cycle_period;
     d.update_period = c.sp_update_period;
@@ -203,7 +205,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.seg_cap = c.seg_capacity;
     d.upd_cap = c.upd_capacity;
     d.seg_reserve = (c.tm_max_lrn_backtrack + 2) * c.sp_num_active;
-    if (d.seg_reserve >= d.seg_cap) return fail(HTM_E_INVALID, "seg_capacity too small for one learning step");
+    if (d.seg_reserve >= d.seg_cap) return htm_fail(HTM_E_INVALID, "seg_capacity too small for one learning step");
     d.n_streams = n;
     d.shared_model = 0;
     d.q_cap = d.seg_cap;
@@ -217,7 +219,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
         size_t q = avail0 > fixed ? (avail0 - fixed) * 2 / 9 : 0;
         q = q / 64 * 64;
         if (q > 1024) q = 1024;
-        if (q < 64) return fail(HTM_E_INVALID, "LDS budget %zu too small for the phase-2 buckets", lds_budget);
+        if (q < 64) return htm_fail(HTM_E_INVALID, "LDS budget %zu too small for the phase-2 buckets", lds_budget);
         d.q_lds = (int32_t)q;
     }
     // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
@@ -248,9 +250,9 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
 static int dalloc(htm_engine* e, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
     hipError_t err = hipMalloc(p, bytes);
-    if (err != hipSuccess) return fail(HTM_E_HIP, "hipMalloc(%zu): %s", bytes, hipGetErrorString(err));
+    if (err != hipSuccess) return htm_fail(HTM_E_HIP, "hipMalloc(%zu): %s", bytes, hipGetErrorString(err));
     err = hipMemset(*p, 0, bytes);
-    if (err != hipSuccess) return fail(HTM_E_HIP, "hipMemset: %s", hipGetErrorString(err));
+    if (err != hipSuccess) return htm_fail(HTM_E_HIP, "hipMemset: %s", hipGetErrorString(err));
     e->allocs.push_back(*p);
     e->bytes += bytes;
     return HTM_OK;
@@ -340,14 +342,14 @@ static int check_lds(const DevCfg& d) {
         for (int fz = 0; fz < 2; fz++) {
             if (learn && fz) continue;
             size_t b = tm_step_lds_bytes(d, learn, fz);
-            if (b > (size_t)maxlds) return fail(HTM_E_INVALID, "TM kernel needs %zu B LDS > %d", b, maxlds);
+            if (b > (size_t)maxlds) return htm_fail(HTM_E_INVALID, "TM kernel needs %zu B LDS > %d", b, maxlds);
         }
     return HTM_OK;
 }
 
 static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out,
                          int32_t fleet_q_cap = 0) {
-    if (!cfg || !out || n_streams < 1) return fail(HTM_E_INVALID, "bad arguments");
+    if (!cfg || !out || n_streams < 1) return htm_fail(HTM_E_INVALID, "bad arguments");
     *out = nullptr;
     HIP_TRY(hipSetDevice(device));
     htm_engine* e = new htm_engine();
@@ -388,7 +390,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (!r && tm_configure_lds(e->dc)) {
         size_t mx = std::max(tm_step_lds_bytes(e->dc, 0, 1),
                              std::max(tm_step_lds_bytes(e->dc, 1, 0), tm_step_lds_bytes(e->dc, 0, 0)));
-        if (mx > 65536) r = fail(HTM_E_HIP, "cannot raise the dynamic LDS limit to %zu B", mx);
+        if (mx > 65536) r = htm_fail(HTM_E_HIP, "cannot raise the dynamic LDS limit to %zu B", mx);
     }
     if (r) {
         for (void* p : e->allocs) (void)hipFree(p);
@@ -401,23 +403,31 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
 
 extern "C" {
 
+// NuPIC initialisation of a created engine (SP pools/permanences, TM RNG)
+static int init_streams(htm_engine* e, const htm_config* cfg, int32_t n_streams, uint64_t** dseeds) {
+    std::vector<uint64_t> seeds((size_t)n_streams);
+    for (int s = 0; s < n_streams; s++) seeds[s] = cfg->sp_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
+    HIP_TRY(hipMemcpy(e->sp.seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
+    if (launch_sp_init(e->dc, e->sp, n_streams, 0)) return htm_fail(HTM_E_HIP, "sp_init launch failed");
+    for (int s = 0; s < n_streams; s++) seeds[s] = cfg->tm_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
+    HIP_TRY(hipMalloc(dseeds, seeds.size() * 8));
+    HIP_TRY(hipMemcpy(*dseeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
+    if (launch_tm_init(e->dc, e->tm, *dseeds, n_streams, 0)) return htm_fail(HTM_E_HIP, "tm_init launch failed");
+    HIP_TRY(hipDeviceSynchronize());
+    return HTM_OK;
+}
+
 int htm_create(const htm_config* cfg, int32_t n_streams, int32_t device, htm_engine** out) {
     int r = create_uninit(cfg, n_streams, device, out);
     if (r) return r;
-    htm_engine* e = *out;
-    std::vector<uint64_t> seeds((size_t)n_streams);
-    for (int s = 0; s < n_streams; s++) seeds[s] = cfg->sp_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
-    hipError_t err = hipMemcpy(e->sp.seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice);
-    if (err != hipSuccess) return fail(HTM_E_HIP, "seed upload: %s", hipGetErrorString(err));
-    if (launch_sp_init(e->dc, e->sp, n_streams, 0)) return fail(HTM_E_HIP, "sp_init launch failed");
-    for (int s = 0; s < n_streams; s++) seeds[s] = cfg->tm_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
     uint64_t* dseeds = nullptr;
-    HIP_TRY(hipMalloc(&dseeds, seeds.size() * 8));
-    HIP_TRY(hipMemcpy(dseeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
-    if (launch_tm_init(e->dc, e->tm, dseeds, n_streams, 0)) return fail(HTM_E_HIP, "tm_init launch failed");
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipFree(dseeds));
-    return HTM_OK;
+    r = init_streams(*out, cfg, n_streams, &dseeds);
+    if (dseeds) (void)hipFree(dseeds);
+    if (r) {  // no half-initialised handle escapes: free everything, *out = NULL
+        htm_destroy(*out);
+        *out = nullptr;
+    }
+    return r;
 }
 
 int htm_destroy(htm_engine* e) {
@@ -432,9 +442,9 @@ int htm_destroy(htm_engine* e) {
 }
 
 int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
-    if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
     if (e->fleet && (sp_learn || tm_learn))
-        return fail(HTM_E_STATE, "a fleet engine shares one frozen model: learning stays off");
+        return htm_fail(HTM_E_STATE, "a fleet engine shares one frozen model: learning stays off");
     e->sp_learn = sp_learn ? 1 : 0;
     if (tm_learn && !e->tm_learn) e->fx_valid = false;
     e->tm_learn = tm_learn ? 1 : 0;
@@ -442,7 +452,7 @@ int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
 }
 
 int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
-    if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
     if (opt == HTM_OPT_FROZEN_INDEX) e->use_frozen = value ? 1 : 0;
     else if (opt == HTM_OPT_KEEP_PREV) e->keep_prev = value ? 1 : 0;
     else if (opt == HTM_OPT_KEEP_OVERLAPS) e->keep_overlaps = value ? 1 : 0;
@@ -453,14 +463,14 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
     }
     else if (opt == HTM_OPT_FUSED) e->fused = value ? 1 : 0;
     else if (opt == HTM_OPT_RUN_CHUNK) {
-        if (value < 1) return fail(HTM_E_INVALID, "run chunk must be >= 1");
+        if (value < 1) return htm_fail(HTM_E_INVALID, "run chunk must be >= 1");
         e->run_chunk = value;
     }
     else if (opt == HTM_OPT_RUN_UNIT) {
-        if (value < 0) return fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
+        if (value < 0) return htm_fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
         e->run_unit = value;
     }
-    else return fail(HTM_E_INVALID, "unknown option %d", opt);
+    else return htm_fail(HTM_E_INVALID, "unknown option %d", opt);
     return HTM_OK;
 }
 
@@ -484,7 +494,7 @@ static int build_fx(htm_engine* e, hipStream_t st) {
     const DevCfg& d = e->dc;
     int ra = alloc_fx(e);
     if (ra) return ra;
-    if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return fail(HTM_E_HIP, "fx count launch");
+    if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return htm_fail(HTM_E_HIP, "fx count launch");
     std::vector<uint64_t> counts((size_t)e->nm);
     HIP_TRY(hipMemcpyAsync(counts.data(), e->d_counts, counts.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -504,7 +514,7 @@ static int build_fx(htm_engine* e, hipStream_t st) {
     }
     HIP_TRY(hipMemsetAsync(e->tm.fx_ent, 0xFF, (size_t)tot * 16, st));
     HIP_TRY(hipMemcpyAsync(e->tm.fx_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
-    if (launch_tm_fx_fill(d, e->tm, e->nm, st)) return fail(HTM_E_HIP, "fx fill launch");
+    if (launch_tm_fx_fill(d, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "fx fill launch");
     HIP_TRY(hipStreamSynchronize(st));
     e->fx_valid = true;
     return HTM_OK;
@@ -558,13 +568,13 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     const int32_t unit = e->run_unit > 0 ? e->run_unit : std::max(16, std::min(64, n_steps / 8));
     if (launch_htm_run(e->dc, e->tm, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
-        return fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
+        return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
 }
 
 int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
-    if (!e || !d_values || !d_scores) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e || !d_values || !d_scores) return htm_fail(HTM_E_INVALID, "bad arguments");
     hipStream_t st = (hipStream_t)stream;
     int frozen = 0;
     int r = prepare_step(e, st, &frozen);
@@ -577,14 +587,14 @@ int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* strea
         HIP_TRY(hipEventRecord(ev[0], st));
     }
     if (launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st))
-        return fail(HTM_E_HIP, "sp_step launch");
+        return htm_fail(HTM_E_HIP, "sp_step launch");
     if (e->keep_prev) {
         // prevPredictedColumns (nonzero colConfidence before compute)
-        if (launch_prev_pred(e->dc, e->tm, e->n, st)) return fail(HTM_E_HIP, "prev_pred launch");
+        if (launch_prev_pred(e->dc, e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "prev_pred launch");
     }
     if (e->profile) HIP_TRY(hipEventRecord(ev[1], st));
     if (launch_tm_step(e->dc, e->tm, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
-        return fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
+        return htm_fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
 }
@@ -592,7 +602,7 @@ int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* strea
 // Kernel times of the profiled steps since the last read:
 // out4 = {SP kernel ms, TM kernel ms, steps, 0}
 int htm_profile_read(htm_engine* e, double* out4) {
-    if (!e || !out4) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e || !out4) return htm_fail(HTM_E_INVALID, "bad arguments");
     HIP_TRY(hipDeviceSynchronize());
     double sp = 0.0, tm = 0.0;
     for (size_t k = 0; k + 2 < e->ev_used + 1 && k < e->ev_used; k += 3) {
@@ -617,7 +627,7 @@ int htm_profile_read(htm_engine* e, double* out4) {
 // calls, inferBacktracks, learnPhase2 calls, learnBacktracks, live segments,
 // pool high-water marks, OR of error flags}
 int htm_counters(htm_engine* e, uint64_t* out8) {
-    if (!e || !out8) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e || !out8) return htm_fail(HTM_E_INVALID, "bad arguments");
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
@@ -636,8 +646,8 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
 }
 
 int htm_debug_stamps(htm_engine* e, uint64_t* out48) {
-    if (!e || !out48) return fail(HTM_E_INVALID, "bad arguments");
-    if (!e->tm.dbg) return fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
+    if (!e || !out48) return htm_fail(HTM_E_INVALID, "bad arguments");
+    if (!e->tm.dbg) return htm_fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
     HIP_TRY(hipDeviceSynchronize());
     const int W = 2 * HTM_NSTAMP;
     std::vector<uint64_t> h((size_t)e->n * W);
@@ -650,8 +660,8 @@ int htm_debug_stamps(htm_engine* e, uint64_t* out48) {
 }
 
 int htm_run(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, void* stream) {
-    if (!e) return fail(HTM_E_INVALID, "null engine");
-    if (n_steps < 0 || (n_steps > 0 && (!d_values || !d_scores))) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (n_steps < 0 || (n_steps > 0 && (!d_values || !d_scores))) return htm_fail(HTM_E_INVALID, "bad arguments");
     const size_t stride = (size_t)e->n * e->cfg.n_fields;
     if (e->fused) {
         hipStream_t st = (hipStream_t)stream;
@@ -725,10 +735,10 @@ size_t htm_output_bytes(const htm_engine* e, int32_t which) {
 }
 
 int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void* stream) {
-    if (!e || !d_dst) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e || !d_dst) return htm_fail(HTM_E_INVALID, "bad arguments");
     size_t per = htm_output_bytes(e, which);
-    if (!per) return fail(HTM_E_INVALID, "unknown output %d", which);
-    if (bytes < per * e->n) return fail(HTM_E_INVALID, "output buffer too small (%zu < %zu)", bytes, per * e->n);
+    if (!per) return htm_fail(HTM_E_INVALID, "unknown output %d", which);
+    if (bytes < per * e->n) return htm_fail(HTM_E_INVALID, "output buffer too small (%zu < %zu)", bytes, per * e->n);
     hipStream_t st = (hipStream_t)stream;
     const DevCfg& d = e->dc;
     switch (which) {
@@ -736,7 +746,7 @@ int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void
         case HTM_OUT_PREV_PRED_COLS:
         case HTM_OUT_TM_OUTPUT:
             if (which == HTM_OUT_PREV_PRED_COLS && !e->keep_prev)
-                return fail(HTM_E_STATE, "prev-predicted columns need htm_set_option(KEEP_PREV)");
+                return htm_fail(HTM_E_STATE, "prev-predicted columns need htm_set_option(KEEP_PREV)");
             hipLaunchKernelGGL(out_kernel, dim3(e->n), dim3(256), 0, st, d, e->sp, e->tm, which, (uint8_t*)d_dst);
             HIP_TRY(hipGetLastError());
             return HTM_OK;
@@ -753,11 +763,11 @@ int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void
             HIP_TRY(hipMemcpyAsync(d_dst, e->tm.colconf, per * e->n, hipMemcpyDeviceToDevice, st));
             return HTM_OK;
         case HTM_OUT_SP_OVERLAPS:
-            if (!e->keep_overlaps) return fail(HTM_E_STATE, "SP overlaps need htm_set_option(KEEP_OVERLAPS)");
+            if (!e->keep_overlaps) return htm_fail(HTM_E_STATE, "SP overlaps need htm_set_option(KEEP_OVERLAPS)");
             HIP_TRY(hipMemcpyAsync(d_dst, e->sp.overlaps, per * e->n, hipMemcpyDeviceToDevice, st));
             return HTM_OK;
     }
-    return fail(HTM_E_INVALID, "unknown output");
+    return htm_fail(HTM_E_INVALID, "unknown output");
 }
 
 size_t htm_state_bytes(const htm_engine* e, int32_t region) {
@@ -772,9 +782,9 @@ static int32_t region_count(const htm_engine* e, int32_t region) {
 
 int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void* h_dst, size_t bytes) {
     if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
-        return fail(HTM_E_INVALID, "bad export arguments");
+        return htm_fail(HTM_E_INVALID, "bad export arguments");
     const Region& r = e->regions[region];
-    if (bytes < r.per_stream * n) return fail(HTM_E_INVALID, "export buffer too small");
+    if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "export buffer too small");
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(h_dst, (uint8_t*)r.base + r.per_stream * s0, r.per_stream * n, hipMemcpyDeviceToHost));
     return HTM_OK;
@@ -782,9 +792,9 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
 
 int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes) {
     if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
-        return fail(HTM_E_INVALID, "bad import arguments");
+        return htm_fail(HTM_E_INVALID, "bad import arguments");
     const Region& r = e->regions[region];
-    if (bytes < r.per_stream * n) return fail(HTM_E_INVALID, "import buffer too small");
+    if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "import buffer too small");
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy((uint8_t*)r.base + r.per_stream * s0, h_src, r.per_stream * n, hipMemcpyHostToDevice));
     if (region >= HTM_ST_TM_HEADER) e->fx_valid = false;
@@ -792,8 +802,8 @@ int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const
 }
 
 int htm_reset_tm(htm_engine* e, void* stream) {
-    if (!e) return fail(HTM_E_INVALID, "null engine");
-    if (launch_tm_reset(e->dc, e->tm, e->n, (hipStream_t)stream)) return fail(HTM_E_HIP, "reset launch");
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (launch_tm_reset(e->dc, e->tm, e->n, (hipStream_t)stream)) return htm_fail(HTM_E_HIP, "reset launch");
     return HTM_OK;
 }
 
@@ -825,19 +835,19 @@ static int replicate_region(uint8_t* base, size_t per, int32_t src, int32_t n, h
 }
 
 int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
-    if (!e || src < 0 || src >= e->n) return fail(HTM_E_INVALID, "bad source stream");
+    if (!e || src < 0 || src >= e->n) return htm_fail(HTM_E_INVALID, "bad source stream");
     hipStream_t st = (hipStream_t)stream;
     for (int id = 1; id <= 16; id++) {
         const Region& r = e->regions[id];
         if (!r.base) continue;
         const int32_t cnt = region_count(e, id);
         if (cnt < 2) continue;
-        if (replicate_region((uint8_t*)r.base, r.per_stream, src, cnt, st)) return fail(HTM_E_HIP, "replicate launch");
+        if (replicate_region((uint8_t*)r.base, r.per_stream, src, cnt, st)) return htm_fail(HTM_E_HIP, "replicate launch");
     }
     // SP active list of the last step too (the TM reads it)
     if (replicate_region((uint8_t*)e->sp.act, HTM_MAXACT * 2, src, e->n, st) ||
         replicate_region((uint8_t*)e->sp.nact, 4, src, e->n, st))
-        return fail(HTM_E_HIP, "replicate launch");
+        return htm_fail(HTM_E_HIP, "replicate launch");
     HIP_TRY(hipStreamSynchronize(st));
     e->fx_valid = false;
     return HTM_OK;
@@ -845,9 +855,9 @@ int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
 
 int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_streams, int32_t q_capacity,
                      int32_t device, htm_engine** out) {
-    if (!model || !out || n_streams < 1 || q_capacity < 64) return fail(HTM_E_INVALID, "bad arguments");
-    if (model->fleet) return fail(HTM_E_INVALID, "the model must be an ordinary engine, not a fleet");
-    if (model_stream < 0 || model_stream >= model->n) return fail(HTM_E_INVALID, "bad model stream");
+    if (!model || !out || n_streams < 1 || q_capacity < 64) return htm_fail(HTM_E_INVALID, "bad arguments");
+    if (model->fleet) return htm_fail(HTM_E_INVALID, "the model must be an ordinary engine, not a fleet");
+    if (model_stream < 0 || model_stream >= model->n) return htm_fail(HTM_E_INVALID, "bad model stream");
     *out = nullptr;
     HIP_TRY(hipSetDevice(model->device));
     HIP_TRY(hipDeviceSynchronize());
@@ -859,17 +869,17 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
         const Region& src = model->regions[id];
         const Region& dst = e->regions[id];
         if (!src.base || !dst.base || src.per_stream != dst.per_stream) {
-            r = fail(HTM_E_STATE, "region %d layout differs", id);
+            r = htm_fail(HTM_E_STATE, "region %d layout differs", id);
             break;
         }
         if (hipMemcpy(dst.base, (const uint8_t*)src.base + src.per_stream * model_stream, src.per_stream,
                       hipMemcpyDefault) != hipSuccess)
-            r = fail(HTM_E_HIP, "fleet copy of region %d", id);
+            r = htm_fail(HTM_E_HIP, "fleet copy of region %d", id);
     }
     if (!r && (hipMemcpy(e->sp.act, model->sp.act + (size_t)model_stream * HTM_MAXACT, HTM_MAXACT * 2,
                          hipMemcpyDefault) != hipSuccess ||
                hipMemcpy(e->sp.nact, model->sp.nact + model_stream, 4, hipMemcpyDefault) != hipSuccess))
-        r = fail(HTM_E_HIP, "fleet copy of the SP output");
+        r = htm_fail(HTM_E_HIP, "fleet copy of the SP output");
     if (!r) r = htm_replicate_stream(e, 0, nullptr);
     if (r) {
         htm_destroy(e);
@@ -885,7 +895,7 @@ int32_t htm_is_fleet(const htm_engine* e) { return e && e->fleet ? 1 : 0; }
 int32_t htm_n_streams(const htm_engine* e) { return e ? e->n : 0; }
 
 int htm_get_config(const htm_engine* e, htm_config* out) {
-    if (!e || !out) return fail(HTM_E_INVALID, "bad arguments");
+    if (!e || !out) return htm_fail(HTM_E_INVALID, "bad arguments");
     *out = e->cfg;
     return HTM_OK;
 }
@@ -900,12 +910,12 @@ int32_t htm_abi_version(void) { return HTM_ABI_VERSION; }
 
 // Synchronise and report per-stream error flags (pool/queue overflow).
 int htm_status(htm_engine* e) {
-    if (!e) return fail(HTM_E_INVALID, "null engine");
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
     for (int s = 0; s < e->n; s++) {
-        if (h[s].error) return fail(HTM_E_CAPACITY, "stream %d error flags 0x%x (1: segment pool full, 2: update queue full, 4: >1 learn-predicted cell, 8: learn-active list overflow)", s, h[s].error);
+        if (h[s].error) return htm_fail(HTM_E_CAPACITY, "stream %d error flags 0x%x (1: segment pool full -- new segments were dropped, raise seg_capacity; 2: segment-update queue full; 4: >1 learn-predicted cell in a column; 8: learn-active cell list overflow; 16: qualifying-segment list overflow, results invalid -- raise q_capacity)", s, h[s].error);
     }
     return HTM_OK;
 }
@@ -913,10 +923,10 @@ int htm_status(htm_engine* e) {
 // ---------------------------------------------------------------------------
 // save / load: "HTMAMD01", abi, config, n, learning flags, then regions
 int htm_save(htm_engine* e, const char* path) {
-    if (!e || !path) return fail(HTM_E_INVALID, "bad arguments");
-    if (e->fleet) return fail(HTM_E_STATE, "fleet engines are not saved: save the model engine they were built from");
+    if (!e || !path) return htm_fail(HTM_E_INVALID, "bad arguments");
+    if (e->fleet) return htm_fail(HTM_E_STATE, "fleet engines are not saved: save the model engine they were built from");
     FILE* f = std::fopen(path, "wb");
-    if (!f) return fail(HTM_E_IO, "cannot open %s", path);
+    if (!f) return htm_fail(HTM_E_IO, "cannot open %s", path);
     const char magic[8] = {'H', 'T', 'M', 'A', 'M', 'D', '0', '1'};
     int32_t abi = HTM_ABI_VERSION;
     bool ok = std::fwrite(magic, 8, 1, f) == 1 && std::fwrite(&abi, 4, 1, f) == 1 &&
@@ -933,14 +943,14 @@ int htm_save(htm_engine* e, const char* path) {
     }
     // last SP output (the TM of the next step does not need it, kept for outputs)
     std::fclose(f);
-    if (!ok) return fail(HTM_E_IO, "write failed: %s", path);
+    if (!ok) return htm_fail(HTM_E_IO, "write failed: %s", path);
     return HTM_OK;
 }
 
 int htm_load(const char* path, int32_t device, htm_engine** out) {
-    if (!path || !out) return fail(HTM_E_INVALID, "bad arguments");
+    if (!path || !out) return htm_fail(HTM_E_INVALID, "bad arguments");
     FILE* f = std::fopen(path, "rb");
-    if (!f) return fail(HTM_E_IO, "cannot open %s", path);
+    if (!f) return htm_fail(HTM_E_IO, "cannot open %s", path);
     char magic[8];
     int32_t abi = 0, n = 0, spl = 1, tml = 1;
     htm_config cfg;
@@ -950,7 +960,7 @@ int htm_load(const char* path, int32_t device, htm_engine** out) {
               std::fread(&spl, 4, 1, f) == 1 && std::fread(&tml, 4, 1, f) == 1;
     if (!ok) {
         std::fclose(f);
-        return fail(HTM_E_IO, "%s is not an engine file of ABI %d", path, HTM_ABI_VERSION);
+        return htm_fail(HTM_E_IO, "%s is not an engine file of ABI %d", path, HTM_ABI_VERSION);
     }
     htm_engine* e = nullptr;
     int r = create_uninit(&cfg, n, device, &e);
@@ -972,7 +982,7 @@ int htm_load(const char* path, int32_t device, htm_engine** out) {
     std::fclose(f);
     if (!ok) {
         htm_destroy(e);
-        return fail(HTM_E_IO, "truncated or inconsistent engine file %s", path);
+        return htm_fail(HTM_E_IO, "truncated or inconsistent engine file %s", path);
     }
     e->sp_learn = spl;
     e->tm_learn = tml;

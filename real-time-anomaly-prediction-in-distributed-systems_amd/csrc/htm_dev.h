@@ -296,6 +296,9 @@ __device__ __forceinline__ float pow_det(float b, uint32_t e) {
     return (float)r;
 }
 
+// sets htm_last_error()'s message and returns code (engine.cpp)
+int htm_fail(int code, const char* fmt, ...);
+
 // host launch wrappers (defined in sp.hip / tm.hip)
 int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st);
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,

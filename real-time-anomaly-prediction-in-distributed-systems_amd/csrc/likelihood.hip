@@ -189,9 +189,9 @@ int htm_likelihood_create(int32_t n_streams, int32_t learning_period, int32_t es
                           int32_t historic_window, int32_t reestimation_period, int32_t device, htm_likelihood** out) {
     if (!out || n_streams < 1 || learning_period < 0 || estimation_samples < 0 || historic_window < 1 ||
         historic_window > LK_HWCAP || reestimation_period < 1)
-        return HTM_E_INVALID;
+        return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     *out = nullptr;
-    if (hipSetDevice(device) != hipSuccess) return HTM_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     htm_likelihood* h = new htm_likelihood();
     h->device = device;
     h->b.lp = learning_period;
@@ -205,7 +205,7 @@ int htm_likelihood_create(int32_t n_streams, int32_t learning_period, int32_t es
     ok = ok && hipMemset(h->b.st, 0, n * sizeof(LkState)) == hipSuccess;
     if (!ok) {
         htm_likelihood_destroy(h);
-        return HTM_E_HIP;
+        return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     }
     *out = h;
     return HTM_OK;
@@ -224,10 +224,10 @@ int htm_likelihood_destroy(htm_likelihood* h) {
 
 int htm_likelihood_step(htm_likelihood* h, const double* d_values, int32_t value_stride, const float* d_scores,
                         double* d_out, void* stream) {
-    if (!h || !d_values || !d_scores || !d_out || value_stride < 1) return HTM_E_INVALID;
+    if (!h || !d_values || !d_scores || !d_out || value_stride < 1) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     hipLaunchKernelGGL(lk_step_kernel, dim3(h->b.n), dim3(256), 0, (hipStream_t)stream, h->b, d_values,
                        value_stride, d_scores, d_out);
-    return hipGetLastError() == hipSuccess ? HTM_OK : HTM_E_HIP;
+    return hipGetLastError() == hipSuccess ? HTM_OK : htm_fail(HTM_E_HIP, "%s: HIP launch/sync failed", __func__);
 }
 
 }  // extern "C"

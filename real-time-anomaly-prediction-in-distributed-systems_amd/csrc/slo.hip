@@ -143,9 +143,9 @@ extern "C" {
 
 int htm_slo_create(int32_t n_streams, double threshold, int32_t max_lead, int32_t slo_response, int32_t device,
                    htm_slo** out) {
-    if (!out || n_streams < 1 || max_lead < 0 || max_lead > SLO_RING - 2) return HTM_E_INVALID;
+    if (!out || n_streams < 1 || max_lead < 0 || max_lead > SLO_RING - 2) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     *out = nullptr;
-    if (hipSetDevice(device) != hipSuccess) return HTM_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     htm_slo* h = new htm_slo();
     h->n = n_streams;
     h->device = device;
@@ -160,7 +160,7 @@ int htm_slo_create(int32_t n_streams, double threshold, int32_t max_lead, int32_
          hipMemset(h->st.rcount, 0, n * 4) == hipSuccess && hipMemset(h->st.acc, 0, n * 7 * 8) == hipSuccess;
     if (!ok) {
         htm_slo_destroy(h);
-        return HTM_E_HIP;
+        return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     }
     *out = h;
     return HTM_OK;
@@ -180,22 +180,22 @@ int htm_slo_destroy(htm_slo* h) {
 
 int htm_slo_record(htm_slo* h, const float* d_scores, int32_t window, const int32_t* d_violations,
                    const int32_t* d_means, const uint8_t* d_valid, void* stream) {
-    if (!h || !d_scores || window < 1 || !d_violations || !d_means) return HTM_E_INVALID;
+    if (!h || !d_scores || window < 1 || !d_violations || !d_means) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     hipLaunchKernelGGL(slo_record_kernel, dim3((h->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->st, h->n,
                        d_scores, window, d_violations, d_means, d_valid, h->threshold, h->max_lead,
                        h->slo_response);
-    return hipGetLastError() == hipSuccess ? HTM_OK : HTM_E_HIP;
+    return hipGetLastError() == hipSuccess ? HTM_OK : htm_fail(HTM_E_HIP, "%s: HIP launch/sync failed", __func__);
 }
 
 int htm_slo_stats(htm_slo* h, int64_t* h_out5, void* stream) {
-    if (!h || !h_out5) return HTM_E_INVALID;
+    if (!h || !h_out5) return htm_fail(HTM_E_INVALID, "%s: invalid argument", __func__);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(slo_stats_kernel, dim3((h->n + 255) / 256), dim3(256), 0, st, h->st, h->n, h->max_lead,
                        h->d_out);
-    if (hipGetLastError() != hipSuccess) return HTM_E_HIP;
+    if (hipGetLastError() != hipSuccess) return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
     if (hipMemcpyAsync(h_out5, h->d_out, (size_t)h->n * 5 * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
-        return HTM_E_HIP;
-    return hipStreamSynchronize(st) == hipSuccess ? HTM_OK : HTM_E_HIP;
+        return htm_fail(HTM_E_HIP, "%s: %s", __func__, hipGetErrorString(hipGetLastError()));
+    return hipStreamSynchronize(st) == hipSuccess ? HTM_OK : htm_fail(HTM_E_HIP, "%s: HIP launch/sync failed", __func__);
 }
 
 }  // extern "C"

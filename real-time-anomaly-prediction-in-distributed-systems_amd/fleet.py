@@ -12,6 +12,8 @@ the input of the SLO alerting (`ModelTesting.py:75-99`).  On ROCm the
 """
 from __future__ import annotations
 
+import numpy as np
+
 
 def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous stream block [s0, s1) of `rank`: the first n_total % world
@@ -100,3 +102,46 @@ class ScoreGather:
         """[world, width] padded blocks -> [n_total] in global stream order."""
         import torch
         return torch.cat([staging[r, : b - a] for r, (a, b) in enumerate(self.ranges)])
+
+
+def max_over_ranks(seconds: float, device=None, group=None) -> float:
+    """The slowest rank's time (the bench contract's max over ranks): one
+    all_reduce(MAX) of a float64 on `device` (CPU tensor for gloo)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(seconds)
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def broadcast_state(engine, regions, src: int = 0, stream: int = 0, device=None, group=None) -> int:
+    """Broadcast stream `stream`'s state from rank `src` into stream `stream`
+    of every other rank's engine: each region exported to host bytes
+    (htm_export_state), packed into ONE uint8 tensor, one `dist.broadcast`
+    (RCCL over xGMI when `device` is a GPU), imported (htm_import_state).
+
+    This is the one-time shared-model distribution of fleet mode (SURVEY.md
+    §5, §8(e)): rank 0 trains the model, the other ranks receive it instead of
+    re-training.  `engine` needs state_bytes / export_state / import_state;
+    `regions` names the regions to send (their sizes agree on every rank,
+    since the engines share a config).  Returns the bytes broadcast."""
+    import torch
+    import torch.distributed as dist
+    sizes = [int(engine.state_bytes(r)) for r in regions]
+    total = sum(sizes)
+    rank = dist.get_rank(group)
+    if rank == src:
+        host = np.concatenate([engine.export_state(r, stream, 1).reshape(-1) for r in regions])
+        buf = torch.from_numpy(host).to(device) if device is not None else torch.from_numpy(host)
+    else:
+        buf = torch.empty(total, dtype=torch.uint8, device=device)
+    dist.broadcast(buf, src=src, group=group)
+    if rank != src:
+        host = buf.cpu().numpy()
+        off = 0
+        for r, n in zip(regions, sizes):
+            engine.import_state(r, host[off:off + n].reshape(1, n), s0=stream)
+            off += n
+    return total

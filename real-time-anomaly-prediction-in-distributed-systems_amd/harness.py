@@ -158,9 +158,11 @@ def model_training(engine, cpu, save_path=None):
     out = torch.empty((n, engine.n_streams), dtype=torch.float32, device=dev)
     k_save = SAVE_FREQUENCY - 1 if (save_path and n >= SAVE_FREQUENCY) else n
     engine.run(vals[:k_save], out=out[:k_save])
+    engine.status()  # raise on pool / queue overflow (NuPIC's NTA_THROW)
     if k_save < n:
         engine.save(save_path)
         engine.run(vals[k_save:], out=out[k_save:])
+        engine.status()
     return out
 
 
@@ -194,4 +196,5 @@ def model_testing(engine, cpu, violations, means, threshold=ANOMALY_SCORE, looka
         for j in range(m):
             slo.record(sc[j * w:(j + 1) * w], vv[j], mm[j])
         windows[r0:r0 + m] = sc.reshape(m, w, n).cpu().numpy()
+        engine.status()  # raise on pool / queue overflow (NuPIC's NTA_THROW)
     return windows, slo.stats()

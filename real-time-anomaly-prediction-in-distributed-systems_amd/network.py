@@ -229,6 +229,21 @@ class Region:
     def getSelf(self):
         return self._impl
 
+    @property
+    def dataSource(self):
+        """Sensor regions: the RecordSensor's data source.  ModelTesting.initModels
+        re-attaches it on the loaded network with
+        `network.regions[_RECORD_SENSOR].dataSource = ds` (ModelTesting.py:176-178)."""
+        if self.type != SENSOR:
+            raise AttributeError("region %s (%s) has no dataSource" % (self.name, self.type))
+        return self._impl.dataSource
+
+    @dataSource.setter
+    def dataSource(self, ds):
+        if self.type != SENSOR:
+            raise AttributeError("region %s (%s) has no dataSource" % (self.name, self.type))
+        self._impl.dataSource = ds
+
     def setParameter(self, name, value):
         if name not in self._MODES[self.type]:
             raise ValueError("region %s (%s) has no settable parameter %r" % (self.name, self.type, name))
@@ -412,6 +427,7 @@ class Network:
         pat = self.engine.get_output("tm_output")
         bucket = f0.bucket_indices(vals[:, 0]) if learn else None
         prob, act = impl.classifier.compute(pat, bucket, vals[:, 0] if learn else None, learn=learn, infer=infer)
+        impl.classifier.status()  # raises like NuPIC on an empty pattern (this record only)
         impl.recordNum += 1
         if infer:
             nb, n = impl.classifier.n_buckets, impl.maxCategoryCount
@@ -448,6 +464,9 @@ class Network:
             sensor.values = vals
             self._scores = self.engine.step(torch.from_numpy(np.ascontiguousarray(vals).ravel()))
             self._run_classifier(vals)
+        # NuPIC raises (NTA_THROW) when a Cells4 pool limit is hit; the engine
+        # records the overflow per stream -- surface it the same way
+        self.engine.status()
 
     def _output(self, region, name):
         if self.engine is None:
@@ -508,6 +527,7 @@ class Network:
         engine.htm (every stream's SP/TM state, htm_save)."""
         self.initialize()
         self._apply_learning()
+        self.engine.status()  # never save a state whose pools overflowed
         os.makedirs(path, exist_ok=True)
         meta = {"n_streams": self.n_streams, "links": self.links, "regions": []}
         for r in self.regions.values():

@@ -65,6 +65,18 @@ def test_record_stream_batches_and_missing_values(rt):
         ds.setData([1, 2])
 
 
+def test_sensor_region_forwards_data_source(rt):
+    # ModelTesting.initModels: network.regions[_RECORD_SENSOR].dataSource = ds (ModelTesting.py:178)
+    net = rt.Network()
+    s = net.addRegion("s", "py.RecordSensor", "{}")
+    sp = net.addRegion("sp", "py.SPRegion", "{}")
+    ds = rt.BatchRecordStream(["cpu"])
+    net.regions["s"].dataSource = ds
+    assert s.getSelf().dataSource is ds and net.regions["s"].dataSource is ds
+    with pytest.raises(AttributeError):
+        sp.dataSource = ds
+
+
 def test_graph_errors_are_raised_before_any_gpu_work(rt):
     net = rt.Network()
     net.addRegion("s", "py.RecordSensor", "{}")
@@ -105,7 +117,8 @@ def test_model1_through_the_facade_matches_golden(rt, traces, tmp_path):
     path = net.save(str(tmp_path / "network1.nta"))
     net2 = rt.Network(path)
     ds2 = rt.BatchRecordStream(["cpu"])
-    net2.regions[ref.SENSOR].getSelf().dataSource = ds2
+    net2.regions[ref.SENSOR].dataSource = ds2  # the reference's own line, ModelTesting.py:178
+    assert net2.regions[ref.SENSOR].getSelf().dataSource is ds2
     tm2 = net2.regions[ref.TMR]
     for r, cpu in enumerate(traces["test"][:40]):
         win = []
