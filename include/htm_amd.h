@@ -124,6 +124,13 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
 #define HTM_OPT_RUN_UNIT 7      /* steps per work-queue unit of a fused htm_run launch (0, the
                                    default: launch steps / 8 clamped to [16, 64]); a stream's
                                    TM state stays in LDS for a unit's steps */
+#define HTM_OPT_BT_ASSIST 8     /* 0 (default) off; 1: in frozen lockstep launches (htm_step), up to 64
+                                   workgroups that finished their own stream replay other streams'
+                                   backtrack start offsets in parallel; 2: the owners run every offset
+                                   through the assisted path themselves.  Results are identical to
+                                   the serial loop in every mode (measured: no faster) */
+#define HTM_OPT_BT_TAIL 9       /* helpers join a launch's backtracks once at most this many owners are
+                                   still running (default 64) */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Kernel times of the profiled launches since the last call (synchronises):

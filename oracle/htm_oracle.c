@@ -473,7 +473,9 @@ typedef struct {
     uint8_t* colmask; /* scratch: active-column membership */
     uint32_t* cand;   /* scratch: candidate cells */
     uint32_t* cand2;
-    int64_t stats[4]; /* inferPhase2 calls, inferBacktracks, lrnPhase2 calls, lrnBacktracks */
+    int64_t stats[5]; /* inferPhase2 calls, inferBacktracks, lrnPhase2 calls, lrnBacktracks,
+                         inferPhase2 calls on the critical path if backtrack start offsets ran in parallel */
+    int bt_crit;      /* scratch: the last inferBacktrack's critical-path phase-2 calls */
     uint32_t variant;
 } tm_t;
 
@@ -1225,17 +1227,20 @@ static void tm_infer_backtrack(const orc_params* p, tm_t* tm) {
     memcpy(tm->infP_backup, tm->infP_t1, nc);
     uint8_t bad[64];
     memset(bad, 0, sizeof(bad));
-    int inSeq = 0, haveCand = 0, candStart = -1;
+    int inSeq = 0, haveCand = 0, candStart = -1, maxlen = 0;
     for (int start = 0; start < numPrev; start++) {
         if (start == cur && haveCand) break;
         inSeq = 0;
+        int len = 0;
         for (int off = start; off < numPrev; off++) {
             memcpy(tm->infP_t1, tm->infP_t, nc);
             inSeq = tm_infer_phase1(tm, tm->inf_pat[off].cols, tm->inf_pat[off].n, off == start);
             if (!inSeq) break;
             inSeq = tm_infer_phase2(p, tm);
+            len++;
             if (!inSeq) break;
         }
+        if (len > maxlen) maxlen = len;
         if (!inSeq) { bad[start] = 1; continue; }
         haveCand = 1;
         candStart = start;
@@ -1246,6 +1251,7 @@ static void tm_infer_backtrack(const orc_params* p, tm_t* tm) {
         memcpy(tm->colConf_cand, tm->colConf_t, (size_t)tm->ncol * 4);
         if (!(tm->variant & ORC_VAR_TM_BT_LAST_START)) break;
     }
+    tm->bt_crit = maxlen + (haveCand ? 0 : 1);
     if (!haveCand) {
         memcpy(tm->infA_t, tm->infA_backup, nc);
         tm_infer_phase2(p, tm);
@@ -1271,12 +1277,15 @@ static void tm_update_inference_state(const orc_params* p, tm_t* tm, const int32
     memcpy(tm->colConf_t1, tm->colConf_t, (size_t)tm->ncol * 4);
     if (p->tm_max_inf_backtrack > 0) pat_push(tm->inf_pat, &tm->n_inf_pat, p->tm_max_inf_backtrack, active, nA);
     int inSeq = tm_infer_phase1(tm, active, nA, tm->reset_called);
+    tm->bt_crit = 0;
     if (!inSeq) {
         tm_infer_backtrack(p, tm);
+        tm->stats[4] += tm->bt_crit;
         return;
     }
     inSeq = tm_infer_phase2(p, tm);
     if (!inSeq) tm_infer_backtrack(p, tm);
+    tm->stats[4] += 1 + tm->bt_crit;
 }
 
 /* BacktrackingTM.compute(bottomUpInput, enableLearn, enableInference=True) */
@@ -1493,7 +1502,7 @@ void orc_tm_scalars(const orc_model* m, int64_t* o) {
 
 double orc_tm_avg_input_density(const orc_model* m) { return m->tm.avg_input_density; }
 
-void orc_tm_stats(const orc_model* m, int64_t* out4) { memcpy(out4, m->tm.stats, sizeof(m->tm.stats)); }
+void orc_tm_stats(const orc_model* m, int64_t* out5) { memcpy(out5, m->tm.stats, sizeof(m->tm.stats)); }
 
 int orc_tm_segments(const orc_model* m, int32_t* info, float* dc, int32_t* src, float* perm, int max_syn) {
     int k = 0;

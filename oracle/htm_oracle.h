@@ -115,8 +115,9 @@ void orc_cell_confidence(const orc_model* m, float* out);
  * n_prev_inf, n_prev_lrn, n_updates, n_segments, n_synapses] */
 void orc_tm_scalars(const orc_model* m, int64_t* out9);
 double orc_tm_avg_input_density(const orc_model* m);
-/* work counters: [inferPhase2 calls, inferBacktracks, lrnPhase2 calls, lrnBacktracks] */
-void orc_tm_stats(const orc_model* m, int64_t* out4);
+/* work counters: [inferPhase2 calls, inferBacktracks, lrnPhase2 calls, lrnBacktracks,
+ * inferPhase2 calls on the critical path were backtrack start offsets replayed in parallel] */
+void orc_tm_stats(const orc_model* m, int64_t* out5);
 /* Segments in canonical order (column, cell, position in cell list).
  * seg_info[k*5+{0..4}] = {cell, isSequence, posActivations, lastDCIter, nsyn}
  * seg_dc[k] = lastPosDutyCycle; syn_src/syn_perm hold max_syn entries per

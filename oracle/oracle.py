@@ -182,10 +182,10 @@ class OracleModel:
         return d
 
     def tm_stats(self) -> dict:
-        out = np.zeros(4, np.int64)
+        out = np.zeros(5, np.int64)
         lib().orc_tm_stats(self.h, _ptr(out))
         return dict(inf_phase2=int(out[0]), inf_backtracks=int(out[1]), lrn_phase2=int(out[2]),
-                    lrn_backtracks=int(out[3]))
+                    lrn_backtracks=int(out[3]), inf_phase2_critical_parallel_bt=int(out[4]))
 
     def tm_segments(self, max_syn: int = 64) -> dict:
         n = lib().orc_tm_segments(self.h, None, None, None, None, max_syn)

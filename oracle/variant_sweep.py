@@ -67,6 +67,10 @@ VARIANTS = {
     "seed 2047": ([], {"seed": 2047}),
     "seed 2048": ([], {"seed": 2048}),
     "seed 2049": ([], {"seed": 2049}),
+    "harness: SP learning off in test, seed 2046": ([], {"sp_learn_test": False, "seed": 2046}),
+    "harness: SP learning off in test, seed 2047": ([], {"sp_learn_test": False, "seed": 2047}),
+    "harness: SP learning off in test, seed 2048": ([], {"sp_learn_test": False, "seed": 2048}),
+    "harness: SP learning off in test, seed 2049": ([], {"sp_learn_test": False, "seed": 2049}),
 }
 
 
@@ -118,11 +122,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--out", default=os.path.join(HERE, "variant_sweep.json"))
-    ap.add_argument("--only", default=None, help="comma-separated subset of variant names")
+    ap.add_argument("--only", default=None, help="';'-separated subset of variant names")
     a = ap.parse_args()
     oracle.build()
     train, test_cpu, means, viol, ref = load_inputs()
-    names = list(VARIANTS) if not a.only else [n for n in VARIANTS if n in a.only.split(",")]
+    names = list(VARIANTS) if not a.only else [n for n in VARIANTS if n in a.only.split(";")]
     work = [(n, VARIANTS[n][0], VARIANTS[n][1]) for n in names]
     out = {"reference": "ML/Data/result_model1.txt", "n_blocks": len(ref), "variants": []}
     with mp.Pool(a.jobs) as pool:

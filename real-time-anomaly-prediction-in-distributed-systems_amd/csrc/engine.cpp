@@ -78,6 +78,11 @@ struct htm_engine {
     int32_t run_chunk = 256;        // steps per fused htm_run launch
     int32_t run_unit = 0;           // steps per work unit of the fused kernel's queue (0: auto)
     uint32_t* wq = nullptr;         // the fused kernel's work queue: next unit + per-stream done blocks
+    int32_t bt_assist = 0;          // HTM_OPT_BT_ASSIST (needs the bt_* buffers); off by default:
+                                    // measured no faster on config 2 (profiles/r02_assist/ab.json)
+    int32_t bt_tail = 64;           // HTM_OPT_BT_TAIL: owners left when helpers join
+    uint32_t bt_epoch = 0;          // last assisted launch's tag
+    unsigned long long bt_base = 0; // workgroups counted by bt_ctl before the next assisted launch
 };
 
 extern "C" {
@@ -299,6 +304,28 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
+    // backtrack assist buffers (frozen lockstep launches): ~16 x 14 KB per
+    // stream of replay results; left out for very large engines (fleets of
+    // 100K+ streams amortise their backtracks over the launch instead)
+    {
+        const size_t rw = 2 * (size_t)d.cw + (size_t)d.ncol;
+        const size_t per = HTM_MAXPAT * (rw * 4 + 16 + 8 + HTM_MAXACT * 2) + 16 + BT_INFO_WORDS * 4;
+        if (S * per <= ((size_t)4 << 30)) {
+            ALLOC(e->tm.bt_state, unsigned long long, S);
+            ALLOC(e->tm.bt_take, unsigned long long, S);
+            ALLOC(e->tm.bt_claim, unsigned long long, S * HTM_MAXPAT);
+            ALLOC(e->tm.bt_res, uint32_t, S * HTM_MAXPAT * rw);
+            ALLOC(e->tm.bt_meta, uint32_t, S * HTM_MAXPAT * 4);
+            ALLOC(e->tm.bt_pat, uint16_t, S * HTM_MAXPAT * HTM_MAXACT);
+            ALLOC(e->tm.bt_info, uint32_t, S * BT_INFO_WORDS);
+            ALLOC(e->tm.bt_ctl, unsigned long long, 4);
+        } else {
+            e->tm.bt_state = nullptr;
+            e->tm.bt_take = e->tm.bt_claim = e->tm.bt_ctl = nullptr;
+            e->tm.bt_res = e->tm.bt_meta = e->tm.bt_info = nullptr;
+            e->tm.bt_pat = nullptr;
+        }
+    }
 #ifdef HTM_STAMPS
     ALLOC(e->tm.dbg, uint64_t, S * 2 * HTM_NSTAMP);
 #endif
@@ -466,6 +493,8 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         if (value < 1) return htm_fail(HTM_E_INVALID, "run chunk must be >= 1");
         e->run_chunk = value;
     }
+    else if (opt == HTM_OPT_BT_ASSIST) e->bt_assist = value < 0 ? 0 : value > 2 ? 2 : value;
+    else if (opt == HTM_OPT_BT_TAIL) e->bt_tail = value < 0 ? 0 : value > 0xFFFFFF ? 0xFFFFFF : value;
     else if (opt == HTM_OPT_RUN_UNIT) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
         e->run_unit = value;
@@ -566,8 +595,21 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     // the launch's tail (measured on config 2, profiles/r01_s4/ab_unit.txt:
     // 256-step launches best at 32, 2324-step launches flat over 48..96)
     const int32_t unit = e->run_unit > 0 ? e->run_unit : std::max(16, std::min(64, n_steps / 8));
-    if (launch_htm_run(e->dc, e->tm, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
-                       e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
+    // backtrack assist: frozen one-step (lockstep) launches; the kernel counts
+    // its workgroups in bt_ctl on top of `base`
+    BtArgs bt{};
+    TmBufs tb = e->tm;
+    if (frozen && n_steps == 1 && e->bt_assist && e->tm.bt_state) {
+        bt.epoch = ++e->bt_epoch;
+        // helpers (1) join once at most bt_tail owners are left; 2: owners only (A/B)
+        bt.pad = e->bt_assist == 1 ? (1u | ((uint32_t)e->bt_tail << 8)) : 0u;
+        bt.base = e->bt_base;
+        e->bt_base += (unsigned long long)e->n;
+    } else {
+        tb.bt_state = nullptr;  // the kernel's "off" test
+    }
+    if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
+                       e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, bt, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;

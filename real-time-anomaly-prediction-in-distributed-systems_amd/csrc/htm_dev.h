@@ -122,6 +122,30 @@ struct TmBufs {
     uint16_t* fx_pcell;     // [S][fx_pcap] cell of each pid
     uint32_t* fx_np;        // [S] number of pids (> fx_pcap: pid lists not built, rows are read)
     uint64_t* dbg;          // [S][32] phase stamps + event counts (HTM_STAMPS builds only, else null)
+    // backtrack assist (frozen lockstep launches): a stream whose step needs
+    // _inferBacktrack posts its pattern history; workgroups that finished
+    // their own stream replay other start offsets of posted jobs in parallel
+    // (the replays are independent while the TM is frozen); the owner takes
+    // the first in-sequence start in NuPIC's order.  Null when not allocated.
+    unsigned long long* bt_state;  // [S] job word: epoch << 16 | numPrev (BT_CLOSED: done)
+    unsigned long long* bt_take;   // [S] next start a helper takes: epoch << 16 | k
+    unsigned long long* bt_claim;  // [S][HTM_MAXPAT] epoch << 2 | 1 claimed, 2 done in sequence, 3 done failed
+    uint32_t* bt_res;              // [S][HTM_MAXPAT][2 * cw + ncol] infA, infP, colConfidence of an in-sequence replay
+    uint32_t* bt_meta;             // [S][HTM_MAXPAT][4] replay's bytes (lo, hi), phase-2 calls, error flags
+    uint16_t* bt_pat;              // [S][HTM_MAXPAT][HTM_MAXACT] posted pattern history (oldest first)
+    uint32_t* bt_info;             // [S][BT_INFO_WORDS] numPrev, lrn_iter, avg density (2 words), lengths
+    unsigned long long* bt_ctl;    // [3] workgroups started, owners done, helper slots taken (monotonic)
+};
+
+#define BT_INFO_WORDS (4 + HTM_MAXPAT)
+#define BT_HELPERS 64  // finished workgroups that stay to help per launch
+#define BT_CLOSED 0xFFFFull
+
+// launch arguments of the backtrack assist (epoch 0: off)
+struct BtArgs {
+    uint32_t epoch;               // launch tag, > 0 and distinct per assisted launch
+    uint32_t pad;                 // bit 0: finished workgroups help (else owners replay every offset)
+    unsigned long long base;      // bt_ctl counts of the earlier assisted launches (n per launch)
 };
 
 // Diagnostic phase stamps (HTM_STAMPS builds only): thread 0 charges the
@@ -308,7 +332,7 @@ int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* sc
                    int n, hipStream_t st);
 int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
                    int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
-                   uint32_t* wq, int unit_steps, hipStream_t st);
+                   uint32_t* wq, int unit_steps, BtArgs bt, hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

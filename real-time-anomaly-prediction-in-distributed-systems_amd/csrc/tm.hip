@@ -89,6 +89,8 @@ struct Tm {
     const uint2* fxrec;
     const uint16_t* fxpcell;
     uint32_t np;       // predictive-capable segments (pids) of this stream
+    const TmBufs* tb;  // the engine's buffers (backtrack assist)
+    uint32_t bt_epoch; // > 0: this launch's backtracks are assisted (frozen lockstep)
 };
 
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
@@ -1007,6 +1009,170 @@ __device__ __forceinline__ const uint16_t* lrn_pat(Tm& t, int k) {
 }
 __device__ __forceinline__ int lrn_len(Tm& t, int k) { return t.sh->lrn_len[(t.sh->lrn_head + k) % HTM_MAXPAT]; }
 
+// ---------------------------------------------------------------------------
+// Backtrack assist.  _inferBacktrack tries start offsets oldest first and
+// takes the first whose replay (start cells at that pattern, then phase 1/2
+// through the current one) stays in sequence.  While the TM is frozen each
+// replay is a pure function of the pattern history and the model (the only
+// writes, the segments' dutyCycle cache, store the value every replay
+// computes), so the replays can run concurrently: the owner posts its history,
+// workgroups that finished their own stream take start offsets 1, 2, ..., and
+// the owner walks the offsets in NuPIC's order, running the ones nobody took
+// itself and waiting for the others.  The result (and the work counters, which
+// count exactly the replays the serial loop runs) equals the serial loop's.
+//
+// Hand-offs follow the agent-scope release/acquire recipe of
+// MI355X_MICROARCH.md (every storing wave waits vmcnt(0), barrier, lane-0
+// release fence, vmcnt(0), relaxed flag store; the reader polls relaxed, then
+// one acquire fence before any load of the handed-off bytes).
+
+__device__ __forceinline__ void bt_release_store(unsigned long long* w, unsigned long long v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool bt_try_claim(unsigned long long* w, uint32_t epoch) {
+    const unsigned long long old = atomicMax(w, ((unsigned long long)epoch << 2) | 1ull);
+    return old < ((unsigned long long)epoch << 2);
+}
+
+// replay patterns [start, numPrev) of the history from start cells at `start`
+// (the inner loop of _inferBacktrack); final state in infA / infP / colconf
+template <bool FROZEN>
+__device__ __forceinline__ bool bt_replay(Tm& t, int start, int numPrev) {
+    bool inSeq = false;
+    for (int off = start; off < numPrev; off++) {
+        wg_copy(t.infP1, t.infP, t.c.cw);
+        __syncthreads();
+        inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
+        if (!inSeq) break;
+        inSeq = infer_phase2<FROZEN>(t);
+        if (!inSeq) break;
+    }
+    return inSeq;
+}
+
+template <bool FROZEN>
+__device__ __forceinline__ void infer_backtrack_assisted(Tm& t, int numPrev, uint32_t* bkA, uint32_t* bkP) {
+    TmSh* sh = t.sh;
+    const DevCfg& c = t.c;
+    const int cw = c.cw;
+    const int cur = numPrev - 1;
+    const TmBufs& b = *t.tb;
+    const uint32_t ep = t.bt_epoch;
+    const size_t s = (size_t)t.s;
+    const size_t rw = 2 * (size_t)cw + (size_t)c.ncol;
+    uint32_t bad = 0;
+    int candStart = -1;
+    // ---- start offset 0 by the owner, unposted: most backtracks lock on there,
+    // and helpers would only burn the CU time the slow owners need
+    if (bt_replay<FROZEN>(t, 0, numPrev)) {
+        candStart = 0;
+    } else {
+        bad = 1u;
+    }
+    const bool post = candStart < 0 && numPrev > 1;
+    if (post) {
+    // ---- post the job: history oldest first, lengths, lrn_iter, avg density
+    uint16_t* jp = b.bt_pat + s * HTM_MAXPAT * HTM_MAXACT;
+    uint32_t* ji = b.bt_info + s * BT_INFO_WORDS;
+    for (int i = threadIdx.x; i < numPrev * HTM_MAXACT; i += TM_NT) {
+        const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
+        if (a < inf_len(t, k)) jp[i] = inf_pat(t, k)[a];
+    }
+    if (threadIdx.x < numPrev) ji[4 + threadIdx.x] = (uint32_t)inf_len(t, threadIdx.x);
+    if (threadIdx.x == 0) {
+        ji[0] = (uint32_t)numPrev;
+        ji[1] = sh->lrn_iter;
+        const unsigned long long ad = (unsigned long long)__double_as_longlong(sh->avg_dens);
+        ji[2] = (uint32_t)ad;
+        ji[3] = (uint32_t)(ad >> 32);
+        // helpers take offsets 2, 3, ...; the owner goes on with 1
+        __hip_atomic_store(&b.bt_take[s], ((unsigned long long)ep << 16) | 2ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    bt_release_store(&b.bt_state[s], ((unsigned long long)ep << 16) | (unsigned long long)numPrev);
+    }
+    // ---- walk the remaining start offsets in NuPIC's order
+    for (int start = 1; post && start < numPrev; start++) {
+        unsigned long long* cl = b.bt_claim + s * HTM_MAXPAT + start;
+        if (threadIdx.x == 0) sh->ti[4] = bt_try_claim(cl, ep) ? 1 : 0;
+        __syncthreads();
+        const bool mine = sh->ti[4] != 0;
+        __syncthreads();
+        bool inSeq;
+        if (mine) {
+            inSeq = bt_replay<FROZEN>(t, start, numPrev);
+            if (threadIdx.x == 0)  // helpers never wait for it: mark it done for them
+                __hip_atomic_store(cl, ((unsigned long long)ep << 2) | (inSeq ? 2ull : 3ull), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (threadIdx.x == 0) {
+                unsigned long long v;
+                for (;;) {
+                    v = __hip_atomic_load(cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((v >> 2) == ep && (v & 3ull) >= 2ull) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                sh->ti[4] = (int)(v & 3ull);
+            }
+            __syncthreads();
+            inSeq = sh->ti[4] == 2;
+            // the helper's replay counts as the serial loop's work
+            const uint32_t* mt = b.bt_meta + (s * HTM_MAXPAT + start) * 4;
+            if (threadIdx.x == 0) {
+                sh->bytes += (unsigned long long)mt[0] | ((unsigned long long)mt[1] << 32);
+                sh->st[0] += mt[2];
+                sh->err |= mt[3];
+            }
+            if (inSeq) {
+                const uint32_t* rs = b.bt_res + (s * HTM_MAXPAT + start) * rw;
+                wg_copy(t.infA, rs, cw);
+                wg_copy(t.infP, rs + cw, cw);
+                wg_copy(reinterpret_cast<uint32_t*>(t.colconf), rs + 2 * cw, c.ncol);
+            }
+            __syncthreads();
+        }
+        if (inSeq) {
+            candStart = start;
+            break;
+        }
+        bad |= 1u << start;
+    }
+    // ---- close the job (helpers stop taking its offsets)
+    if (post && threadIdx.x == 0)
+        __hip_atomic_store(&b.bt_state[s], ((unsigned long long)ep << 16) | BT_CLOSED, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (candStart < 0) {
+        wg_copy(t.infA, bkA, cw);
+        __syncthreads();
+        (void)infer_phase2<FROZEN>(t);
+    }
+    if (threadIdx.x == 0) {
+        int npop = 0;
+        for (int i = 0; i < numPrev; i++) {
+            if (((bad >> i) & 1u) || (candStart >= 0 && i <= candStart)) npop++;
+            else break;
+        }
+        sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
+        sh->n_inf_pat -= npop;
+        // scratch traffic: backup out + in, the posted history
+        sh->bytes += 2ull * 4ull * cw + 4ull * cw + (candStart < 0 ? 4ull * cw : 0ull) +
+                     (post ? 2ull * numPrev * HTM_MAXACT : 0ull);
+    }
+    wg_copy(t.infP1, bkP, cw);
+    __syncthreads();
+    (void)cur;
+}
+
 // _inferBacktrack(activeColumns)
 template <bool FROZEN>
 __device__ __forceinline__ void infer_backtrack(Tm& t) {
@@ -1023,6 +1189,11 @@ __device__ __forceinline__ void infer_backtrack(Tm& t) {
     wg_copy(bkA, t.infA, cw);
     wg_copy(bkP, t.infP1, cw);
     __syncthreads();
+    if (FROZEN && t.bt_epoch) {
+        infer_backtrack_assisted<FROZEN>(t, numPrev, bkA, bkP);
+        STAMP(t, SB_BT);
+        return;
+    }
     uint32_t bad = 0;
     bool haveCand = false;
     int candStart = -1;
@@ -1764,15 +1935,13 @@ __device__ __forceinline__ void compact_pool(Tm& t) {
 // ---------------------------------------------------------------------------
 // One BacktrackingTM.compute + raw anomaly of stream s by the calling
 // workgroup (TM_NT threads), LDS at `lds` (tm_layout).
+// Bind the LDS regions and stream s's buffers: the model (SP, segment pool,
+// frozen index) of stream s (the fleet's shared instance), the per-stream
+// scratch (qualifying lists, backtrack backups) of stream `scr` -- a helper
+// replaying another stream's backtrack uses its own scratch.
 template <bool LEARN, bool FROZEN>
-// first / last: the step opens / closes a run of steps by this workgroup.
-// Between them the stream's TM state (cell bitmaps, colConfidence, header,
-// pattern history, RNG) stays in LDS: only the first step loads it from HBM
-// and only the last writes it back.
-__device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores,
-                                             int keep_prev, int s, uint8_t* lds, int first = 1, int last = 1) {
+__device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b, int s, int scr, uint8_t* lds) {
     const TmLayout L = tm_layout(c, LEARN, FROZEN);
-    Tm t;
     t.c = c;
     t.s = s;
     t.sh = reinterpret_cast<TmSh*>(lds);
@@ -1799,10 +1968,10 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     t.duty = b.seg_duty + ms * sc * 3;
     t.nseg = b.cell_nseg + ms * c.ncells;
     t.upd = b.upd + ms * c.upd_cap;
-    t.sbm = b.scr_bm + (size_t)s * 5 * c.cw;
-    t.sconf = b.scr_conf + (size_t)s * c.ncol;
-    t.q1 = b.scr_q + (size_t)s * c.q_cap;
-    t.q2 = b.scr_q2 + (size_t)s * c.q_cap;
+    t.sbm = b.scr_bm + (size_t)scr * 5 * c.cw;
+    t.sconf = b.scr_conf + (size_t)scr * c.ncol;
+    t.q1 = b.scr_q + (size_t)scr * c.q_cap;
+    t.q2 = b.scr_q2 + (size_t)scr * c.q_cap;
     if (FROZEN) {
         t.fxoff = b.fx_off + ms * (size_t)c.fx_noff;
         t.fxent = b.fx_ent + b.fx_base[ms];
@@ -1816,6 +1985,21 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         t.fxpcell = nullptr;
         t.np = 0;
     }
+    t.tb = &b;
+    t.bt_epoch = 0;
+}
+
+template <bool LEARN, bool FROZEN>
+// first / last: the step opens / closes a run of steps by this workgroup.
+// Between them the stream's TM state (cell bitmaps, colConfidence, header,
+// pattern history, RNG) stays in LDS: only the first step loads it from HBM
+// and only the last writes it back.  bt_epoch > 0: backtracks are assisted.
+__device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores,
+                                             int keep_prev, int s, uint8_t* lds, int first = 1, int last = 1,
+                                             uint32_t bt_epoch = 0) {
+    Tm t;
+    tm_bind<LEARN, FROZEN>(t, c, b, s, s, lds);
+    t.bt_epoch = bt_epoch;
     TmSh* sh = t.sh;
 #ifdef HTM_STAMPS
     if (threadIdx.x == 0) {
@@ -2072,10 +2256,129 @@ __global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBu
 // quantisation of n streams over the resident slots.  State handed between
 // units goes through HBM: agent-scope fences on both sides (the XCDs' L2s
 // are not coherent with each other).
+// A workgroup that finished its own stream helps with posted backtrack jobs:
+// it takes a start offset of an open job (bt_take), claims it (bt_claim),
+// replays it with its own LDS and scratch, and publishes the result.  It
+// returns when every owner of the launch is done -- or, while workgroups of
+// the launch still wait to be dispatched, as soon as it finds nothing to do
+// (its slot is theirs).  Owners never wait on an unclaimed offset, so no
+// wait depends on a workgroup that is not running.
+template <bool FROZEN>
+__device__ __forceinline__ void bt_helper(const DevCfg& c, const TmBufs& b, uint8_t* lds, const BtArgs& bt, int n,
+                                          int my_s) {
+    TmSh* sh = reinterpret_cast<TmSh*>(lds);
+    const uint32_t ep = bt.epoch;
+    const unsigned long long all = bt.base + (unsigned long long)n;
+    const size_t rw = 2 * (size_t)c.cw + (size_t)c.ncol;
+    for (;;) {
+        if (wave_id() == 0) {
+            int job = -1, k = -1, state = 0;
+            const unsigned long long done = __hip_atomic_load(&b.bt_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (done >= all) {
+                state = 2;
+            } else {
+                const unsigned long long started =
+                    __hip_atomic_load(&b.bt_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                state = started >= all ? 1 : 0;
+                // help only in the launch's tail (at most `tail` owners left): earlier,
+                // helpers share CUs with running owners and slow them more than they help
+                const unsigned long long tail = bt.pad >> 8;
+                const bool in_tail = state == 1 && all - done <= tail;
+                for (int base = 0; in_tail && base < n && job < 0; base += 64) {
+                    const int j = base + lane_id();
+                    const int sj = j < n ? (my_s + 1 + j) % n : 0;
+                    const unsigned long long v =
+                        j < n ? __hip_atomic_load(&b.bt_state[sj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                    const uint32_t npj = (uint32_t)(v & 0xFFFFull);
+                    uint64_t bal = __ballot(j < n && (uint32_t)(v >> 16) == ep && (v & 0xFFFFull) != BT_CLOSED);
+                    while (bal && job < 0) {
+                        const int l0 = __ffsll((unsigned long long)bal) - 1;
+                        bal &= bal - 1ull;
+                        const int cand = __shfl(sj, l0, 64);
+                        const uint32_t np = __shfl(npj, l0, 64);
+                        int kk = -1;
+                        if (lane_id() == 0) {
+                            // the job's words were published before its state: acquire them
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            for (;;) {
+                                const unsigned long long tk = atomicAdd(&b.bt_take[cand], 1ull);
+                                const uint32_t x = (uint32_t)(tk & 0xFFFFull);
+                                if ((uint32_t)(tk >> 16) != ep || x >= np || x >= HTM_MAXPAT) break;
+                                if (bt_try_claim(&b.bt_claim[(size_t)cand * HTM_MAXPAT + x], ep)) {
+                                    kk = (int)x;
+                                    break;
+                                }
+                            }
+                        }
+                        kk = __shfl(kk, 0, 64);
+                        if (kk >= 0) {
+                            job = cand;
+                            k = kk;
+                        }
+                    }
+                }
+            }
+            if (lane_id() == 0) {
+                sh->ti[5] = job;
+                sh->ti[6] = k;
+                sh->ti[7] = state;
+            }
+        }
+        __syncthreads();
+        const int job = sh->ti[5], k = sh->ti[6], state = sh->ti[7];
+        __syncthreads();
+        if (job < 0) {
+            if (state != 1) return;  // all owners done, or dispatch still pending: leave
+            if (threadIdx.x == 0) __builtin_amdgcn_s_sleep(127);
+            __syncthreads();
+            continue;
+        }
+        // ---- replay start offset k of stream `job` (model of job, scratch of my_s)
+        Tm t;
+        tm_bind<false, FROZEN>(t, c, b, job, my_s, lds);
+        const uint32_t* ji = b.bt_info + (size_t)job * BT_INFO_WORDS;
+        const uint16_t* jp = b.bt_pat + (size_t)job * HTM_MAXPAT * HTM_MAXACT;
+        const int np = (int)ji[0];
+        if (threadIdx.x == 0) {
+            sh->lrn_iter = ji[1];
+            sh->avg_dens = __longlong_as_double((long long)((unsigned long long)ji[2] | ((unsigned long long)ji[3] << 32)));
+            sh->n_inf_pat = np;
+            sh->inf_head = 0;
+            sh->bytes = 0;
+            sh->st[0] = 0;
+            sh->err = 0;
+        }
+        if (threadIdx.x < HTM_MAXPAT) sh->inf_len[threadIdx.x] = threadIdx.x < np ? (uint16_t)ji[4 + threadIdx.x] : 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < np * HTM_MAXACT; i += TM_NT) {
+            const int kk = i / HTM_MAXACT, a = i % HTM_MAXACT;
+            if (a < sh->inf_len[kk]) sh->inf_pat[kk][a] = jp[i];
+        }
+        __syncthreads();
+        const bool inSeq = bt_replay<FROZEN>(t, k, np);
+        const size_t slot = (size_t)job * HTM_MAXPAT + k;
+        if (inSeq) {
+            uint32_t* rs = b.bt_res + slot * rw;
+            wg_copy(rs, t.infA, c.cw);
+            wg_copy(rs + c.cw, t.infP, c.cw);
+            wg_copy(rs + 2 * c.cw, reinterpret_cast<const uint32_t*>(t.colconf), c.ncol);
+        }
+        if (threadIdx.x == 0) {
+            uint32_t* mt = b.bt_meta + slot * 4;
+            mt[0] = (uint32_t)sh->bytes;
+            mt[1] = (uint32_t)(sh->bytes >> 32);
+            mt[2] = sh->st[0];
+            mt[3] = sh->err;
+        }
+        bt_release_store(&b.bt_claim[slot], ((unsigned long long)ep << 2) | (inSeq ? 2ull : 3ull));
+    }
+}
+
 template <bool LEARN, bool FROZEN>
 __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
                                              float* scores, int n_steps, int sp_learn, int keep_prev,
-                                             int keep_overlaps, uint32_t* wq, int unit_steps, int n) {
+                                             int keep_overlaps, uint32_t* wq, int unit_steps, int n, BtArgs bt) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t unit_sh[3];  // unit, its stream, its block
     SpShared& ssh = *reinterpret_cast<SpShared*>(lds + tm_layout(c, LEARN, FROZEN).off_U);
@@ -2086,6 +2389,9 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
     // one unit per stream (n_steps <= unit_steps, e.g. every htm_step): no
     // hand-offs, so no queue and no fences -- workgroup b runs stream b
     const bool direct = nblk == 1;
+    // backtrack assist: frozen single-step (lockstep) launches only
+    const uint32_t bt_ep = (FROZEN && direct && b.bt_state) ? bt.epoch : 0u;
+    if (bt_ep && threadIdx.x == 0) atomicAdd(&b.bt_ctl[0], 1ull);
     uint32_t u = 0xFFFFFFFFu;
     int s = 0, k = 0, k0 = 0, k1 = 0;
     for (;;) {
@@ -2131,9 +2437,21 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
         else sp_step_body<false>(c, sp, v, s, ssh, keep_overlaps);
         __syncthreads();
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
-                                    k == k1 - 1);
+                                    k == k1 - 1, bt_ep);
         __syncthreads();
         k++;
+    }
+    if (bt_ep && blockIdx.x < (uint32_t)n) {
+        __shared__ uint32_t stay;
+        if (threadIdx.x == 0) {
+            atomicAdd(&b.bt_ctl[1], 1ull);  // this owner is done
+            // the first BT_HELPERS finishers stay as helpers; the others leave at
+            // once (a crowd of idle pollers costs the owners more than it helps)
+            const unsigned long long slot = atomicAdd(&b.bt_ctl[2], 1ull) - bt.base;  // every owner counts
+            stay = (bt.pad & 1u) && slot < BT_HELPERS ? 1u : 0u;
+        }
+        __syncthreads();
+        if (stay) bt_helper<FROZEN>(c, b, lds, bt, n, (int)blockIdx.x);
     }
 }
 
@@ -2145,8 +2463,8 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #endif
 #define HTM_RUN_ARGS                                                                                          \
     DevCfg c, TmBufs b, SpBufs sp, const double *values, float *scores, int n_steps, int sp_learn, int keep_prev, \
-        int keep_overlaps, uint32_t *wq, int unit_steps, int n
-#define HTM_RUN_PASS c, b, sp, values, scores, n_steps, sp_learn, keep_prev, keep_overlaps, wq, unit_steps, n
+        int keep_overlaps, uint32_t *wq, int unit_steps, int n, BtArgs bt
+#define HTM_RUN_PASS c, b, sp, values, scores, n_steps, sp_learn, keep_prev, keep_overlaps, wq, unit_steps, n, bt
 
 __global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_kernel(
     HTM_RUN_ARGS) {
@@ -2180,7 +2498,7 @@ static int run_grid(const void* fn, size_t lds, int total) {
 
 int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
                    int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
-                   uint32_t* wq, int unit_steps, hipStream_t st) {
+                   uint32_t* wq, int unit_steps, BtArgs bt, hipStream_t st) {
     if (n <= 0 || n_steps <= 0) return 0;
     if (unit_steps < 1) unit_steps = 1;
     size_t lds = tm_step_lds_bytes(c, tm_learn, frozen);

@@ -7,6 +7,7 @@ are not expected: this is a sanity band, documented as such.  What IS pinned
 exactly: every score is float32(k/40) with 40 active columns
 and the harness arithmetic (float32 score vs double threshold).
 """
+import json
 import os
 
 import numpy as np
@@ -17,6 +18,13 @@ from conftest import GOLDEN
 # (threshold, TP, FP, TN, FN) from ML/Data/result_model1.txt:206-209 (0.5),
 # :426-429 (0.85), :451-454 (0.9)
 REFERENCE = [(0.5, 16, 465, 1785, 8), (0.85, 10, 161, 2094, 9), (0.9, 4, 108, 2139, 23)]
+
+
+def sweep_blocks():
+    """The reference's 101 threshold blocks (tests/golden/result_model1_sweep.json,
+    extracted from ML/Data/result_model1.txt by tests/golden/make_traces.py)."""
+    with open(os.path.join(GOLDEN, "result_model1_sweep.json")) as f:
+        return json.load(f)["blocks"]
 
 
 @pytest.fixture(scope="module")
@@ -60,3 +68,68 @@ def test_train_fixture_prefix_reproduces(oracle_mod, golden, traces):
         assert s == golden["train_scores"][k]
         if k < 300:
             assert np.array_equal(m.active_columns(), golden["train_active"][k])
+
+
+def test_reference_sweep_moves_only_at_float32_k_over_40():
+    """SURVEY.md §0.4 on the reference's own data: wherever the reference's
+    counts change between adjacent thresholds a < b, a score float32(k/40)
+    lies in (a, b] (the harness alarms on score > T, ModelTesting.py:76).
+    Float64 k/40 scores would put no score in 11 of those intervals."""
+    blocks = [b for b in sweep_blocks() if not b["excluded"]]
+    f32 = [float(np.float32(k / 40.0)) for k in range(41)]
+    f64 = [k / 40.0 for k in range(41)]
+    changes, miss64 = 0, 0
+    for a, b in zip(blocks, blocks[1:]):
+        ca = (a["tp"], a["fp"], a["tn"], a["fn"])
+        cb = (b["tp"], b["fp"], b["tn"], b["fn"])
+        if ca == cb:
+            continue
+        changes += 1
+        lo, hi = a["threshold"], b["threshold"]
+        assert any(lo < s <= hi for s in f32), (lo, hi)
+        miss64 += not any(lo < s <= hi for s in f64)
+    assert changes >= 30 and miss64 >= 10
+
+
+# The documented band of the full curve (DESIGN.md §2, oracle/variant_sweep.json):
+# the off-repo sweep is not reproducible exactly (unknown NuPIC build and random
+# draws; the seed ensemble alone moves the curve by this much or more), so the
+# test pins the regime and the known gap, on every one of the 100 blocks.
+BAND_SPLIT = 0.45      # operating range: the code's 0.85 and the README's 0.98 / 0.99
+BAND_HI_REL = 0.30     # T >= 0.45: |alarms - ref| <= 0.30 ref + 15
+BAND_HI_ABS = 15
+BAND_HI_TP = 8         # T >= 0.45: |TP - ref TP| <= 8
+BAND_LO_RATIO = 2.0    # T < 0.45: ref <= alarms <= 2.0 ref (the restatement predicts
+                       # fewer windows perfectly: 112 all-zero windows vs the reference's 725)
+
+
+def test_full_sweep_in_documented_band(golden, traces):
+    import slo_reference
+    w = golden["test_windows"]
+    for b in sweep_blocks():
+        if b["excluded"]:
+            continue  # the 0.0 block is all-alarm, unreachable with '>' (SURVEY.md §4)
+        t = b["threshold"]
+        tp, fp, tn, fn, _ = slo_reference.evaluate(w, traces["test_mean"], traces["test_violations"], t)
+        assert tp + fp + tn + fn == 2274
+        alarms, ref_alarms = tp + fp, b["tp"] + b["fp"]
+        if t >= BAND_SPLIT:
+            assert abs(alarms - ref_alarms) <= BAND_HI_REL * ref_alarms + BAND_HI_ABS, (t, alarms, ref_alarms)
+            assert abs(tp - b["tp"]) <= BAND_HI_TP, (t, tp, b["tp"])
+        else:
+            assert ref_alarms <= alarms <= BAND_LO_RATIO * ref_alarms, (t, alarms, ref_alarms)
+
+
+def test_slo_labels_differ_from_the_reference_sweep(traces):
+    """Model-independent pin: at threshold 1.0 nothing alarms, so TN/FN depend
+    only on the SLO labels.  ModelTesting.py's rule (mean >= 70 or violations
+    > 0, :57-60) on the committed TestingData.txt labels 72 records as
+    within-lead-time positives (15 violating records: rows 0-16 and
+    1579-1583); the reference's sweep reports 53 (TN 2221 / FN 53,
+    result_model1.txt:501-502).  Its sweep did not label the committed data the
+    way the committed harness does -- the TP/FN part of the gap is not the model's."""
+    import slo_reference
+    w0 = np.zeros((len(traces["test_mean"]), 8), np.float32)
+    assert slo_reference.evaluate(w0, traces["test_mean"], traces["test_violations"], 1.0)[:4] == (0, 0, 2202, 72)
+    last = [b for b in sweep_blocks() if b["threshold"] == 1.0][0]
+    assert (last["tn"], last["fn"]) == (2221, 53)

@@ -21,7 +21,7 @@ T = int(os.environ.get("STAMP_STEPS", "200"))
 d = np.load(os.path.join(ROOT, "tests", "golden", "model1_traces.npz"))
 train = [c for c, m in zip(d["train_cpu"], d["train_mem"]) if not (np.isnan(c) or np.isnan(m))][:2184]
 trace = d["test_cpu"].astype(np.float64)
-eng, _, hdr = bench.trained_engine(rt, N, 72 * 1024, 0, train)
+eng, _, hdr, _ = bench.trained_engine(rt, N, 72 * 1024, 0, train)
 eng.set_learning(False, False)
 vals = torch.tensor(bench.make_inputs(N, 0, N, 0, T + 16, trace), device="cuda")
 for k in range(16):
