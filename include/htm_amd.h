@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HTM_ABI_VERSION 1
+#define HTM_ABI_VERSION 2
 
 /* error codes */
 #define HTM_OK 0
@@ -95,6 +95,12 @@ typedef struct {
     int32_t upd_capacity;        /* queued segment updates per stream */
     int32_t seed_stride;         /* stream s uses seeds sp_seed + s*stride,
                                     tm_seed + s*stride (0: all identical) */
+    /* > 0: the SP reads an external input SDR of sdr_bits bits instead of the
+     * encoder -- the second level of the reference's Models 2/3, whose L2
+     * SPRegion is fed the L1 TMRegion's bottomUpOut (MultiLevelNetworkModel.py:92-97,
+     * MultiLevelNetworkAnomaly.py:112-116); steps go through htm_step_sdr /
+     * htm_run_sdr.  <= 32768 */
+    int32_t sdr_bits;
 } htm_config;
 
 typedef struct htm_engine htm_engine;
@@ -162,6 +168,13 @@ int htm_step(htm_engine* eng, const double* d_values, float* d_scores, void* str
 /* Run n_steps steps back to back: d_values is [n_steps][n_streams][n_fields],
  * d_scores is [n_steps][n_streams]. */
 int htm_run(htm_engine* eng, int32_t n_steps, const double* d_values, float* d_scores, void* stream);
+
+/* The same for an engine whose SP reads an input SDR (sdr_bits > 0): d_sdr is a
+ * DEVICE uint32 bitmap [n_streams][ceil(sdr_bits/32)] (e.g. another engine's
+ * HTM_OUT_TM_OUTPUT: L1 TM bottomUpOut -> L2 SPRegion bottomUpIn,
+ * MultiLevelNetworkModel.py:94), or [n_steps][n_streams][words] for htm_run_sdr. */
+int htm_step_sdr(htm_engine* eng, const uint32_t* d_sdr, float* d_scores, void* stream);
+int htm_run_sdr(htm_engine* eng, int32_t n_steps, const uint32_t* d_sdr, float* d_scores, void* stream);
 
 /* Output selectors for htm_get_output (all per stream, concatenated over
  * streams, written to a DEVICE buffer of `bytes` bytes on `stream`). */

@@ -230,7 +230,7 @@ static float sp_density(const orc_params* p, const sp_t* sp) {
 }
 
 static void sp_init(const orc_params* p, sp_t* sp) {
-    int nin = p->n_fields * p->enc_n, ncol = p->sp_columns;
+    int nin = p->sdr_bits > 0 ? p->sdr_bits : p->n_fields * p->enc_n, ncol = p->sp_columns;
     sp->nin = nin;
     sp->ncol = ncol;
     sp->potential = (uint8_t*)calloc((size_t)ncol * nin, 1);
@@ -1376,9 +1376,9 @@ void orc_default_params(orc_params* p) {
 }
 
 orc_model* orc_create(const orc_params* p) {
-    if (p->tm_max_inf_backtrack > 60 || p->tm_max_lrn_backtrack > 60 ||
+    if (p->sdr_bits < 0 || (p->tm_max_inf_backtrack > 60 || p->tm_max_lrn_backtrack > 60 ||
         p->tm_max_syn_per_seg > ORC_MAXSYN || p->tm_new_syn_count > ORC_MAXSYN ||
-        p->tm_cells_per_col > 64)
+        p->tm_cells_per_col > 64))
         return NULL;
     orc_model* m = (orc_model*)calloc(1, sizeof(orc_model));
     m->p = *p;
@@ -1411,8 +1411,23 @@ void orc_free(orc_model* m) {
     free(m);
 }
 
+static float step_after_encode(orc_model* m, int sp_learn, int tm_learn);
+
 float orc_step(orc_model* m, const double* values, int sp_learn, int tm_learn) {
     enc_encode(&m->p, values, m->input);
+    return step_after_encode(m, sp_learn, tm_learn);
+}
+
+float orc_step_sdr(orc_model* m, const uint8_t* input, int sp_learn, int tm_learn) {
+    for (int i = 0; i < m->sp.nin; i++) m->input[i] = input[i] ? 1 : 0;
+    return step_after_encode(m, sp_learn, tm_learn);
+}
+
+void orc_tm_output(const orc_model* m, uint8_t* out) {
+    for (int k = 0; k < m->tm.ncells; k++) out[k] = (m->tm.infA_t[k] | m->tm.infP_t[k]) ? 1 : 0;
+}
+
+static float step_after_encode(orc_model* m, int sp_learn, int tm_learn) {
     sp_compute(&m->p, &m->sp, m->input, sp_learn);
     /* TMRegion (anomalyMode): prevPredictedColumns = nonzero(topDownCompute())
      * captured before compute */

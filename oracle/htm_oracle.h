@@ -69,6 +69,10 @@ typedef struct {
      * frozen restatement the HIP engine is held bit-exact to).  Only used by
      * oracle/variant_sweep.py to A/B them against ML/Data/result_model1.txt. */
     uint32_t variant;
+    /* > 0: the SP input is an external SDR of this many bits (a second-level SP
+     * fed a TM's bottomUpOut, MultiLevelNetworkModel.py:92-94); the encoder is
+     * unused and steps go through orc_step_sdr */
+    int32_t sdr_bits;
 } orc_params;
 
 #define ORC_VAR_SP_TIE_LOW       0x001u /* global inhibition: ties -> LOWER index (strict '>' admission) */
@@ -97,6 +101,11 @@ float orc_step(orc_model* m, const double* values, int sp_learn, int tm_learn);
 void orc_step_batch(orc_model** models, int n, const double* values,
                     int sp_learn, int tm_learn, float* scores, int n_threads);
 void orc_tm_reset(orc_model* m);
+/* One step of a model whose SP reads an external SDR (sdr_bits > 0):
+ * input[sdr_bits] 0/1 -> SP -> TM -> raw anomaly (NetworkModel-style order) */
+float orc_step_sdr(orc_model* m, const uint8_t* input, int sp_learn, int tm_learn);
+/* TMRegion bottomUpOut (outputType 'normal'): infActive | infPredicted, 0/1 per cell */
+void orc_tm_output(const orc_model* m, uint8_t* out);
 
 /* ---- introspection (state dumps for parity tests) ---- */
 int orc_num_inputs(const orc_model* m);

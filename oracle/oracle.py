@@ -36,7 +36,7 @@ class OrcParams(ctypes.Structure):
         ("tm_pam_length", ctypes.c_int32), ("tm_max_inf_backtrack", ctypes.c_int32),
         ("tm_max_lrn_backtrack", ctypes.c_int32), ("tm_max_seq_length", ctypes.c_int32),
         ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
-        ("variant", ctypes.c_uint32),
+        ("variant", ctypes.c_uint32), ("sdr_bits", ctypes.c_int32),
     ]
 
 
@@ -70,6 +70,9 @@ def lib():
         L.orc_step_batch.argtypes = [P(vp), ctypes.c_int, P(ctypes.c_double), ctypes.c_int, ctypes.c_int,
                                      P(ctypes.c_float), ctypes.c_int]
         L.orc_tm_reset.argtypes = [vp]
+        L.orc_step_sdr.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int]
+        L.orc_step_sdr.restype = ctypes.c_float
+        L.orc_tm_output.argtypes = [vp, vp]
         L.orc_num_inputs.argtypes = [vp]
         L.orc_num_inputs.restype = ctypes.c_int
         L.orc_num_cells.argtypes = [vp]
@@ -140,6 +143,19 @@ class OracleModel:
 
     def tm_reset(self):
         lib().orc_tm_reset(self.h)
+
+    def step_sdr(self, bits, sp_learn: bool, tm_learn: bool) -> np.float32:
+        """One step of a second-level model (sdr_bits > 0) on a 0/1 input SDR."""
+        b = np.ascontiguousarray(np.asarray(bits, dtype=np.uint8).ravel())
+        if b.size != self.n_inputs:
+            raise ValueError("expected %d input bits" % self.n_inputs)
+        return np.float32(lib().orc_step_sdr(self.h, _ptr(b), int(sp_learn), int(tm_learn)))
+
+    def tm_output(self) -> np.ndarray:
+        """TMRegion bottomUpOut: infActive | infPredicted (0/1 per cell)."""
+        out = np.zeros(self.n_cells, np.uint8)
+        lib().orc_tm_output(self.h, _ptr(out))
+        return out
 
     def encode(self, values) -> np.ndarray:
         v = np.ascontiguousarray(np.atleast_1d(np.asarray(values, dtype=np.float64)))

@@ -62,6 +62,7 @@ class HtmConfig(ctypes.Structure):
         ("tm_max_lrn_backtrack", ctypes.c_int32), ("tm_max_seq_length", ctypes.c_int32),
         ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
         ("seg_capacity", ctypes.c_int32), ("upd_capacity", ctypes.c_int32), ("seed_stride", ctypes.c_int32),
+        ("sdr_bits", ctypes.c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -96,7 +97,7 @@ class TmUpdate(ctypes.Structure):
 
 EXPORTED = [
     "htm_default_config", "htm_create", "htm_destroy", "htm_set_learning", "htm_set_option", "htm_status",
-    "htm_step", "htm_run", "htm_get_output", "htm_output_bytes", "htm_state_bytes", "htm_export_state",
+    "htm_step", "htm_run", "htm_step_sdr", "htm_run_sdr", "htm_get_output", "htm_output_bytes", "htm_state_bytes", "htm_export_state",
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
     "htm_profile_read", "htm_counters", "htm_debug_stamps",
@@ -146,6 +147,8 @@ def lib():
     L.htm_status.argtypes = [vp]
     L.htm_step.argtypes = [vp, vp, vp, vp]
     L.htm_run.argtypes = [vp, i32, vp, vp, vp]
+    L.htm_step_sdr.argtypes = [vp, vp, vp, vp]
+    L.htm_run_sdr.argtypes = [vp, i32, vp, vp, vp]
     L.htm_get_output.argtypes = [vp, i32, vp, sz, vp]
     L.htm_output_bytes.argtypes = [vp, i32]
     L.htm_output_bytes.restype = sz

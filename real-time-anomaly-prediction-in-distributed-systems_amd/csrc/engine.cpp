@@ -132,10 +132,16 @@ void htm_default_config(htm_config* c) {
 }  // extern "C"
 
 static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) {
-    if (c.n_fields < 1 || c.n_fields > 4) return htm_fail(HTM_E_INVALID, "n_fields must be 1..4");
-    if (c.enc_w < 1 || c.enc_w >= c.enc_n || c.enc_n * c.n_fields > 2048)
-        return htm_fail(HTM_E_INVALID, "encoder n/w out of range");
-    if (c.n_fields * c.enc_w >= 128) return htm_fail(HTM_E_INVALID, "n_fields*w must be < 128");
+    const bool sdr = c.sdr_bits != 0;
+    if (sdr) {
+        if (c.sdr_bits < 1 || c.sdr_bits > HTM_MAX_SDR)
+            return htm_fail(HTM_E_INVALID, "sdr_bits must be 0 (encoder input) or 1..%d", HTM_MAX_SDR);
+    } else {
+        if (c.n_fields < 1 || c.n_fields > 4) return htm_fail(HTM_E_INVALID, "n_fields must be 1..4");
+        if (c.enc_w < 1 || c.enc_w >= c.enc_n || c.enc_n * c.n_fields > 2048)
+            return htm_fail(HTM_E_INVALID, "encoder n/w out of range");
+        if (c.n_fields * c.enc_w >= 128) return htm_fail(HTM_E_INVALID, "n_fields*w must be < 128");
+    }
     if (c.sp_columns < 64 || c.sp_columns % 64 != 0 || c.sp_columns > 4096)
         return htm_fail(HTM_E_INVALID, "sp_columns must be a multiple of 64 in [64, 4096]");
     if (c.sp_num_active < 1 || c.sp_num_active > HTM_MAXACT) return htm_fail(HTM_E_INVALID, "sp_num_active must be 1..64");
@@ -157,7 +163,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     if (c.seg_capacity < 64 || c.seg_capacity > (1 << 27)) return htm_fail(HTM_E_INVALID, "seg_capacity");
     if (c.upd_capacity < 1 || c.upd_capacity > 65535) return htm_fail(HTM_E_INVALID, "upd_capacity");
     std::memset(&d, 0, sizeof(d));
-    d.n_fields = c.n_fields;
+    d.n_fields = sdr ? 0 : c.n_fields;
     d.enc_n = c.enc_n;
     d.enc_w = c.enc_w;
     d.enc_clip = c.enc_clip;
@@ -165,7 +171,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.enc_max = c.enc_maxval;
     d.enc_resolution = (c.enc_maxval - c.enc_minval) / (double)(c.enc_n - c.enc_w);
     d.enc_halfwidth = (c.enc_w - 1) / 2;
-    d.nin = c.n_fields * c.enc_n;
+    d.nin = sdr ? c.sdr_bits : c.n_fields * c.enc_n;
+    d.sdr_in = sdr ? 1 : 0;
     d.nin_pad = (int32_t)round_up((size_t)d.nin, 32);
     d.ncol = c.sp_columns;
     d.nw = c.sp_columns / 32;
@@ -230,6 +237,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
     // bitonic key sort at Model-1 sizes
     d.fin_mode = 2;
+    d.fx_mode = 0;
+    if (const char* env = std::getenv("HTM_FX_MODE")) d.fx_mode = std::atoi(env) & 7;  // A/B knob
     if (const char* env = std::getenv("HTM_TM_FIN"))
         d.fin_mode = std::strcmp(env, "sorted") == 0 ? 1 : std::strcmp(env, "buckets") == 0 ? 0 : 2;
     // frozen-inference counter window: the union region holds the u8
@@ -240,10 +249,15 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     const size_t cell_words = 64 + (size_t)(d.max_act_cells + 1) / 2 + 2 * (size_t)d.max_act_cells + 1 + FX_OWN / 2;
     size_t avail = lds_budget > off_u ? (lds_budget - off_u) / 4 : 0;
     size_t win = avail > cell_words ? (avail - cell_words) * 4 : 0;
-    win = (win / 1024) * 1024;
+    // 64-slot granularity (counter sweeps work in 16-byte quads): a window a
+    // few hundred slots wider can save a whole pass per phase 2 (config 2:
+    // 68,376 live segments fit 3 windows of 22,976, not of 22,528)
+    size_t gran = 64;
+    if (const char* env = std::getenv("HTM_FX_GRAN")) gran = (size_t)std::max(64, std::atoi(env)) / 64 * 64;  // A/B knob
+    win = (win / gran) * gran;
     if (win < 1024) win = 1024;
     if (win > 64512) win = 64512;
-    size_t capr = round_up((size_t)d.seg_cap, 1024);
+    size_t capr = round_up((size_t)d.seg_cap, 64);
     if (win > capr) win = capr;
     d.fx_win = (int32_t)win;
     d.fx_nwin = (int32_t)((d.seg_cap + d.fx_win - 1) / d.fx_win);
@@ -407,6 +421,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
         budget = (size_t)optin - 2048;
         r = derive(*cfg, n_streams, budget, e->dc);
     }
+    if (!r && e->dc.sdr_in) e->fused = 0;  // SDR input: SP kernel + TM kernel per step
     if (!r && e->fleet) {
         e->dc.shared_model = 1;
         e->dc.q_cap = std::min(fleet_q_cap, e->dc.seg_cap);
@@ -488,7 +503,10 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         e->ev_used = 0;
         e->ev_steps.clear();
     }
-    else if (opt == HTM_OPT_FUSED) e->fused = value ? 1 : 0;
+    else if (opt == HTM_OPT_FUSED) {
+        if (value && e->dc.sdr_in) return htm_fail(HTM_E_INVALID, "SDR-input engines run unfused");
+        e->fused = value ? 1 : 0;
+    }
     else if (opt == HTM_OPT_RUN_CHUNK) {
         if (value < 1) return htm_fail(HTM_E_INVALID, "run chunk must be >= 1");
         e->run_chunk = value;
@@ -615,20 +633,18 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     return HTM_OK;
 }
 
-int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
-    if (!e || !d_values || !d_scores) return htm_fail(HTM_E_INVALID, "bad arguments");
-    hipStream_t st = (hipStream_t)stream;
-    int frozen = 0;
-    int r = prepare_step(e, st, &frozen);
-    if (r) return r;
-    if (e->fused) return run_fused(e, 1, d_values, d_scores, st, frozen);
+// One unfused step: the SP kernel (encoder values or input SDR), then the TM kernel.
+static int step_unfused(htm_engine* e, const double* d_values, const uint32_t* d_sdr, float* d_scores,
+                        hipStream_t st, int frozen) {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    int r;
     if (e->profile) {
         r = next_events(e, ev, 1);
         if (r) return r;
         HIP_TRY(hipEventRecord(ev[0], st));
     }
-    if (launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st))
+    if (d_sdr ? launch_sp_step_sdr(e->dc, e->sp, d_sdr, e->sp_learn, e->n, e->keep_overlaps, st)
+              : launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st))
         return htm_fail(HTM_E_HIP, "sp_step launch");
     if (e->keep_prev) {
         // prevPredictedColumns (nonzero colConfidence before compute)
@@ -638,6 +654,38 @@ int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* strea
     if (launch_tm_step(e->dc, e->tm, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
         return htm_fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
+    return HTM_OK;
+}
+
+int htm_step(htm_engine* e, const double* d_values, float* d_scores, void* stream) {
+    if (!e || !d_values || !d_scores) return htm_fail(HTM_E_INVALID, "bad arguments");
+    if (e->dc.sdr_in) return htm_fail(HTM_E_INVALID, "this engine reads an input SDR: use htm_step_sdr");
+    hipStream_t st = (hipStream_t)stream;
+    int frozen = 0;
+    int r = prepare_step(e, st, &frozen);
+    if (r) return r;
+    if (e->fused) return run_fused(e, 1, d_values, d_scores, st, frozen);
+    return step_unfused(e, d_values, nullptr, d_scores, st, frozen);
+}
+
+int htm_step_sdr(htm_engine* e, const uint32_t* d_sdr, float* d_scores, void* stream) {
+    if (!e || !d_sdr || !d_scores) return htm_fail(HTM_E_INVALID, "bad arguments");
+    if (!e->dc.sdr_in) return htm_fail(HTM_E_INVALID, "this engine reads encoder values: use htm_step");
+    hipStream_t st = (hipStream_t)stream;
+    int frozen = 0;
+    int r = prepare_step(e, st, &frozen);
+    if (r) return r;
+    return step_unfused(e, nullptr, d_sdr, d_scores, st, frozen);
+}
+
+int htm_run_sdr(htm_engine* e, int32_t n_steps, const uint32_t* d_sdr, float* d_scores, void* stream) {
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (n_steps < 0 || (n_steps > 0 && (!d_sdr || !d_scores))) return htm_fail(HTM_E_INVALID, "bad arguments");
+    const size_t stride = (size_t)e->n * (e->dc.nin_pad / 32);
+    for (int32_t k = 0; k < n_steps; k++) {
+        int r = htm_step_sdr(e, d_sdr + (size_t)k * stride, d_scores + (size_t)k * e->n, stream);
+        if (r) return r;
+    }
     return HTM_OK;
 }
 
@@ -703,6 +751,7 @@ int htm_debug_stamps(htm_engine* e, uint64_t* out48) {
 
 int htm_run(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, void* stream) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (e->dc.sdr_in) return htm_fail(HTM_E_INVALID, "this engine reads an input SDR: use htm_run_sdr");
     if (n_steps < 0 || (n_steps > 0 && (!d_values || !d_scores))) return htm_fail(HTM_E_INVALID, "bad arguments");
     const size_t stride = (size_t)e->n * e->cfg.n_fields;
     if (e->fused) {
@@ -899,6 +948,7 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
                      int32_t device, htm_engine** out) {
     if (!model || !out || n_streams < 1 || q_capacity < 64) return htm_fail(HTM_E_INVALID, "bad arguments");
     if (model->fleet) return htm_fail(HTM_E_INVALID, "the model must be an ordinary engine, not a fleet");
+    if (model->dc.sdr_in) return htm_fail(HTM_E_INVALID, "fleets are built from encoder-input engines");
     if (model_stream < 0 || model_stream >= model->n) return htm_fail(HTM_E_INVALID, "bad model stream");
     *out = nullptr;
     HIP_TRY(hipSetDevice(model->device));

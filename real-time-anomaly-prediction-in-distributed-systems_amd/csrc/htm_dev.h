@@ -17,6 +17,7 @@
 #define HTM_MAXK 32       // cells per column
 #define HTM_MAXPAT 16     // backtrack pattern history slots
 #define HTM_NPLANES 7     // bit-sliced overlap planes (overlap <= 127)
+#define HTM_MAX_SDR 32768 // SDR-input SP: input bits (Models 2/3 level 2: 2048 x 12)
 #define HTM_MAXNW 128     // ncol/32 words (ncol <= 4096)
 #ifndef TM_NT
 #define TM_NT 256                  // threads of the TM workgroup (one stream)
@@ -65,6 +66,10 @@ struct DevCfg {
     int32_t n_streams;
     int32_t shared_model;                 // fleet: every stream reads model instance 0 (SP + TM frozen)
     int32_t q_cap;                        // per-stream capacity of the qualifying-segment scratch lists
+    int32_t fx_mode;                      // frozen counting: bit 0 masked padding, bit 1 wave-aggregated
+                                          // qualification (fx_count_block_push); bit 2 rewrite the
+                                          // dutyCycle record on every frozen step (no FX_FRESH)
+    int32_t sdr_in;                       // the SP reads an external input SDR of nin bits (no encoder)
 };
 
 // instance of the model buffers (SP permanences/connections, TM segment
@@ -118,7 +123,7 @@ struct TmBufs {
     uint64_t* fx_base;      // [S] first block of the stream
     uint32_t* fx_off;       // [S][fx_noff]: [cell][window] lists, then [cell] pid lists, then the end
     uint4* fx_ent;          // [total blocks] 8 x u16 entries each
-    uint2* fx_rec;          // [S][seg_cap] {cell, dutyCycle bits}
+    uint2* fx_rec;          // [S][seg_cap] {cell | FX_FRESH, dutyCycle bits}
     uint16_t* fx_pcell;     // [S][fx_pcap] cell of each pid
     uint32_t* fx_np;        // [S] number of pids (> fx_pcap: pid lists not built, rows are read)
     uint64_t* dbg;          // [S][32] phase stamps + event counts (HTM_STAMPS builds only, else null)
@@ -138,6 +143,7 @@ struct TmBufs {
 };
 
 #define BT_INFO_WORDS (4 + HTM_MAXPAT)
+#define FX_FRESH 0x80000000u  // fx_rec.x: the segment's dutyCycle record holds its frozen value
 #define BT_HELPERS 64  // finished workgroups that stay to help per launch
 #define BT_CLOSED 0xFFFFull
 
@@ -327,6 +333,8 @@ int htm_fail(int code, const char* fmt, ...);
 int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st);
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                    hipStream_t st);
+int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,
+                       hipStream_t st);
 int launch_tm_init(const DevCfg& c, const TmBufs& b, const uint64_t* seeds, int n, hipStream_t st);
 int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen,
                    int n, hipStream_t st);

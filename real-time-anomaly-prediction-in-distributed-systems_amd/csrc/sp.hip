@@ -18,59 +18,130 @@
 //     (float32, potential order) and flips connected bits with atomicXor.
 #include "sp_dev.h"
 
+#include <algorithm>
+
 // ---------------------------------------------------------------------------
-// SP initialisation: one lane per stream runs nupic::Random sequentially.
-__global__ void sp_init_kernel(DevCfg c, SpBufs b, int n) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
+// SP initialisation: one lane per stream runs nupic::Random sequentially (the
+// draw order is NuPIC's; draws depend on each other, so the parallelism is
+// across streams).  The 31-word additive generator lives in registers: draw k
+// updates word (3 + k) mod 31 from word k mod 31, so 31 consecutive draws have
+// compile-time indices -- they are generated a block at a time into the lane's
+// LDS buffer and consumed from there.  The column's potential and connected
+// rows are built in the lane's LDS, stored column-major, and a second kernel
+// transposes the connected rows into the input-major bitmap the overlap reads.
+
+// 31 draws starting at phase 0 (draw index k = 0 mod 31): state and outputs
+__device__ __forceinline__ void rng_block(uint32_t (&st)[31], uint32_t* out) {
+#pragma unroll
+    for (int j = 0; j < 31; j++) {
+        const int f = (3 + j) % 31;
+        st[f] += st[j];
+        out[j] = (st[f] >> 1) & 0x7fffffffu;
+    }
+}
+
+__device__ __forceinline__ void rng_seed_reg(uint32_t (&st)[31], uint64_t seed) {
+    int32_t x = (int32_t)(seed % 2147483646ull + 1ull);
+    st[0] = (uint32_t)x;
+#pragma unroll
+    for (int i = 1; i < 31; i++) {
+        const int32_t hi = x / 127773, lo = x % 127773;
+        x = 16807 * lo - 2836 * hi;
+        if (x < 0) x += 2147483647;
+        st[i] = (uint32_t)x;
+    }
+    // 310 burn-in draws = 10 blocks: the phase is 0 again afterwards
+    for (int r = 0; r < 10; r++) {
+#pragma unroll
+        for (int j = 0; j < 31; j++) st[(3 + j) % 31] += st[j];
+    }
+}
+
+struct RegRng {
     uint32_t st[31];
-    int32_t f, r;
-    rng_seed(st, f, r, b.seeds[s]);
+    uint32_t* buf;  // 31 words of LDS owned by the lane
+    int idx;
+    __device__ __forceinline__ uint32_t raw() {
+        if (idx == 31) {
+            rng_block(st, buf);
+            idx = 0;
+        }
+        return buf[idx++];
+    }
+    // Random::getUInt32(max): raw draws are < 2^31 <= the rejection bound
+    __device__ __forceinline__ uint32_t u32(uint32_t max) { return raw() % max; }
+    // Random::getReal64(): getUInt64(2^48) (lo | hi << 32, never rejected) * 2^-48
+    __device__ __forceinline__ double real64() {
+        const uint64_t lo = raw();
+        const uint64_t hi = raw();
+        return (double)((lo | (hi << 32)) & ((1ull << 48) - 1ull)) * (1.0 / 281474976710656.0);
+    }
+};
+
+__global__ void sp_init_kernel(DevCfg c, SpBufs b, uint32_t* connC, int s0, int n) {
+    extern __shared__ uint32_t dyn[];
+    const int pw = c.nin_pad >> 5;
+    const int s = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (s >= n) return;  // no barriers below: lanes are independent
+    uint32_t* lane_lds = dyn + (size_t)threadIdx.x * (32 + 2 * (size_t)pw);
+    RegRng g;
+    rng_seed_reg(g.st, b.seeds[s]);
+    g.buf = lane_lds;
+    g.idx = 31;
+    uint32_t* prow = lane_lds + 32;  // potential pool bits of the column
+    uint32_t* crow = prow + pw;      // connected bits of the column
     // tieBreaker_[i] = 0.01 * getReal64()  (drawn, unused by global inhibition)
-    for (int i = 0; i < c.ncol; i++) (void)rng_real64(st, f, r);
-    const int nin = c.nin, pw = c.nin_pad >> 5;
-    uint32_t* connT = b.connT + (size_t)s * c.nin_pad * c.nw;
+    for (int i = 0; i < c.ncol; i++) (void)g.real64();
+    const int nin = c.nin;
     uint32_t* pot = b.potmask + (size_t)s * c.ncol * pw;
+    uint32_t* cc = connC + (size_t)(s - s0) * c.ncol * pw;
     float* perm = b.perm + (size_t)s * c.ncol * c.n_potential;
     const float span = 1.0f - c.sp_conn;  // synPermMax_ - synPermConnected_
     const float conn = c.sp_conn;
+    const float ratio = (float)nin / (float)c.ncol;
     for (int col = 0; col < c.ncol; col++) {
-        float ratio = (float)nin / (float)c.ncol;
-        float coord = (float)(((double)col + 0.5) * (double)ratio);
-        int32_t center = (int32_t)floorf(coord);
-        uint32_t* prow = pot + (size_t)col * pw;
-        // WrappingNeighborhood(center, radius=nin) order + Knuth selection sampling
-        uint32_t count = (uint32_t)nin;
-        uint32_t k = (uint32_t)c.n_potential, chosen = 0;
+        for (int w = 0; w < pw; w++) prow[w] = crow[w] = 0u;
+        const float coord = (float)(((double)col + 0.5) * (double)ratio);
+        const int32_t center = (int32_t)floorf(coord);
+        // WrappingNeighborhood(center, radius = nin) order + Knuth selection sampling
+        const uint32_t count = (uint32_t)nin;
+        const uint32_t k = (uint32_t)c.n_potential;
+        uint32_t chosen = 0;
+        int32_t in = center % nin;  // (center - nin + i) mod nin at i = 0
         for (uint32_t i = 0; i < count && chosen < k; i++) {
-            if (rng_u32(st, f, r, count - i) < k - chosen) {
-                int32_t in = (center - nin + (int32_t)i) % nin;
-                if (in < 0) in += nin;
+            if (g.u32(count - i) < k - chosen) {
                 prow[in >> 5] |= 1u << (in & 31);
                 chosen++;
             }
+            if (++in == nin) in = 0;
         }
         // initPermanence_ in input order; updatePermanencesForColumn_(raise)
         float* pr = perm + (size_t)col * c.n_potential;
         int rank = 0;
-        for (int i = 0; i < nin; i++) {
-            if (!((prow[i >> 5] >> (i & 31)) & 1u)) continue;
-            float p;
-            if (rng_real64(st, f, r) <= 0.5) {
-                p = conn + (float)((double)span * rng_real64(st, f, r));
-            } else {
-                p = conn * (float)rng_real64(st, f, r);
+        for (int w = 0; w < pw; w++) {
+            for (uint32_t x = prow[w]; x; x &= x - 1) {
+                const int i = w * 32 + __ffs(x) - 1;
+                float p;
+                if (g.real64() <= 0.5) {
+                    p = conn + (float)((double)span * g.real64());
+                } else {
+                    p = conn * (float)g.real64();
+                }
+                p = (float)((double)(int32_t)(p * 100000.0f) / 100000.0);
+                p = p < c.sp_trim ? 0.0f : p;
+                // raisePermanencesToThreshold_: clip [0,1] (stimulus threshold 0 never loops)
+                p = p > 1.0f ? 1.0f : p;
+                p = p < 0.0f ? 0.0f : p;
+                const bool isconn = p >= c.sp_conn_thr;
+                p = p > 1.0f ? 1.0f : p;
+                p = p < c.sp_trim ? 0.0f : p;
+                pr[rank++] = p;
+                if (isconn) crow[i >> 5] |= 1u << (i & 31);
             }
-            p = (float)((double)(int32_t)(p * 100000.0f) / 100000.0);
-            p = p < c.sp_trim ? 0.0f : p;
-            // raisePermanencesToThreshold_: clip [0,1] (stimulus threshold 0 never loops)
-            p = p > 1.0f ? 1.0f : p;
-            p = p < 0.0f ? 0.0f : p;
-            bool isconn = p >= c.sp_conn_thr;
-            p = p > 1.0f ? 1.0f : p;
-            p = p < c.sp_trim ? 0.0f : p;
-            pr[rank++] = p;
-            if (isconn) connT[(size_t)i * c.nw + (col >> 5)] |= 1u << (col & 31);
+        }
+        for (int w = 0; w < pw; w++) {
+            pot[(size_t)col * pw + w] = prow[w];
+            cc[(size_t)col * pw + w] = crow[w];
         }
     }
     uint32_t* sc = b.scalars + (size_t)s * 4;
@@ -80,9 +151,64 @@ __global__ void sp_init_kernel(DevCfg c, SpBufs b, int n) {
     sc[3] = 0;
 }
 
+// connT[s][i][w] bit (col & 31) = connC[s][col][i / 32] bit (i & 31), w = col / 32:
+// one thread per 32 x 32 bit tile (32 column-word loads, a register transpose,
+// 32 input-row-word stores)
+__global__ void sp_conn_transpose_kernel(DevCfg c, SpBufs b, const uint32_t* connC, int s0, int n) {
+    const int pw = c.nin_pad >> 5, nw = c.nw;
+    const size_t tiles = (size_t)nw * pw;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = s0 + (int)(t / tiles);
+    if (s >= n) return;
+    const size_t r = t % tiles;
+    const int w = (int)(r / pw), iw = (int)(r % pw);
+    const uint32_t* src = connC + (size_t)(s - s0) * c.ncol * pw;
+    uint32_t m[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) m[j] = src[(size_t)(w * 32 + j) * pw + iw];  // row j = column w*32+j
+    // transpose: m[j] bit i (input iw*32+i of column w*32+j) -> o[i] bit j
+#pragma unroll
+    for (int sh = 16; sh > 0; sh >>= 1) {
+        const uint32_t mask = sh == 16 ? 0x0000FFFFu : sh == 8 ? 0x00FF00FFu : sh == 4 ? 0x0F0F0F0Fu
+                              : sh == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+        for (int j = 0; j < 32; j++) {
+            if ((j & sh) == 0) {
+                const uint32_t a = m[j], bb = m[j | sh];
+                m[j] = (a & mask) | ((bb & mask) << sh);
+                m[j | sh] = ((a >> sh) & mask) | (bb & ~mask);
+            }
+        }
+    }
+    uint32_t* dst = b.connT + (size_t)s * c.nin_pad * nw;
+#pragma unroll
+    for (int i = 0; i < 32; i++) dst[(size_t)(iw * 32 + i) * nw + w] = m[i];
+}
+
 int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st) {
-    hipLaunchKernelGGL(sp_init_kernel, dim3((n + 63) / 64), dim3(64), 0, st, c, b, n);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    const int pw = c.nin_pad >> 5;
+    // lanes per block: LDS for 32 rng words + two rows of pw words per lane
+    const size_t per_lane = (32 + 2 * (size_t)pw) * 4;
+    int lanes = (int)std::min<size_t>(64, std::max<size_t>(1, 32768 / per_lane));
+    // column-major connected rows, a chunk of streams at a time (<= 1 GiB)
+    const size_t per_stream = (size_t)c.ncol * pw * 4;
+    const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, ((size_t)1 << 30) / per_stream));
+    uint32_t* connC = nullptr;
+    if (hipMalloc(&connC, per_stream * chunk) != hipSuccess) return -1;
+    int rc = 0;
+    for (int s0 = 0; s0 < n && !rc; s0 += chunk) {
+        const int s1 = std::min(n, s0 + chunk);
+        const int m = s1 - s0;
+        hipLaunchKernelGGL(sp_init_kernel, dim3((m + lanes - 1) / lanes), dim3(lanes), per_lane * lanes, st, c, b,
+                           connC, s0, s1);
+        const size_t threads = (size_t)m * c.nw * pw;
+        hipLaunchKernelGGL(sp_conn_transpose_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, c, b,
+                           connC, s0, s1);
+        if (hipGetLastError() != hipSuccess) rc = -1;
+        if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = -1;
+    }
+    (void)hipFree(connC);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -90,6 +216,23 @@ template <bool LEARN>
 __global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps) {
     __shared__ SpShared sh;
     sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps);
+}
+
+// Level-2 SP of Models 2/3 (SPRegion fed an SDR, MultiLevelNetworkModel.py:92-95):
+// the input bitmap is staged in LDS; one workgroup per stream.
+template <bool LEARN>
+__global__ __launch_bounds__(256) void sp_step_sdr_kernel(DevCfg c, SpBufs b, const uint32_t* sdr, int write_overlaps) {
+    __shared__ SpSharedSdr sh;
+    sp_step_body<LEARN>(c, b, sdr, blockIdx.x, sh, write_overlaps);
+}
+
+int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,
+                       hipStream_t st) {
+    if (learn)
+        hipLaunchKernelGGL(sp_step_sdr_kernel<true>, dim3(n), dim3(256), 0, st, c, b, sdr, keep_overlaps);
+    else
+        hipLaunchKernelGGL(sp_step_sdr_kernel<false>, dim3(n), dim3(256), 0, st, c, b, sdr, keep_overlaps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,

@@ -23,7 +23,11 @@ __device__ __forceinline__ int enc_first_on_bit(const DevCfg& c, double x) {
 
 // ---------------------------------------------------------------------------
 // Overlap + global inhibition by wave 0.  Lane l owns words l and l+64.
+//
+// Encoder input (SpShared): <= 2048 input bits, < 128 of them active, so the
+// overlaps fit 7 bit-sliced planes and the active rows are listed.
 struct SpShared {
+    static constexpr int kPlanes = HTM_NPLANES;
     uint32_t in[64];           // input SDR bits (nin_pad <= 2048)
     uint32_t act[HTM_MAXNW];   // active columns bitmap
     uint32_t ovnz[HTM_MAXNW];  // overlap > 0
@@ -35,30 +39,59 @@ struct SpShared {
     int32_t nbump;
     uint16_t bump[HTM_MAXNW * 32 > 4096 ? 4096 : HTM_MAXNW * 32];
     float red[16];  // per-wave maxima (<= 16 waves)
+    template <class F>
+    __device__ __forceinline__ void each_active_input(const DevCfg&, F&& f) const {
+        for (int a = 0; a < n_act_inputs; a++) f(act_inputs[a]);
+    }
 };
 
-__device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SpShared& sh, int write_overlaps) {
+// External SDR input (the second level of Models 2/3: the L1 TM bottomUpOut,
+// up to HTM_MAX_SDR bits, any number of them active): the whole input bitmap
+// sits in LDS and the overlap walks its set bits; 15 planes hold overlaps up
+// to 32767 >= any input width accepted.
+struct SpSharedSdr {
+    static constexpr int kPlanes = 15;
+    uint32_t in[HTM_MAX_SDR / 32];
+    uint32_t act[HTM_MAXNW];
+    uint32_t ovnz[HTM_MAXNW];
+    uint16_t actlist[HTM_MAXACT];
+    int32_t nact;
+    uint32_t iter;
+    int32_t nbump;
+    uint16_t bump[HTM_MAXNW * 32 > 4096 ? 4096 : HTM_MAXNW * 32];
+    float red[16];
+    template <class F>
+    __device__ __forceinline__ void each_active_input(const DevCfg& c, F&& f) const {
+        const int pw = c.nin_pad >> 5;
+        for (int w = 0; w < pw; w++)
+            for (uint32_t x = in[w]; x; x &= x - 1) f(w * 32 + __ffs(x) - 1);
+    }
+};
+
+template <class SH>
+__device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SH& sh, int write_overlaps) {
+    constexpr int NPL = SH::kPlanes;
     const int l = lane_id();
     const int nw = c.nw;
-    uint32_t p0[HTM_NPLANES], p1[HTM_NPLANES];
+    uint32_t p0[NPL], p1[NPL];
 #pragma unroll
-    for (int k = 0; k < HTM_NPLANES; k++) { p0[k] = 0; p1[k] = 0; }
+    for (int k = 0; k < NPL; k++) { p0[k] = 0; p1[k] = 0; }
     const uint32_t* connT = b.connT + (size_t)model_stream(c, s) * c.nin_pad * nw;
-    const int nai = sh.n_act_inputs;
-    for (int a = 0; a < nai; a++) {
-        const uint32_t* row = connT + (size_t)sh.act_inputs[a] * nw;
+    // bit-sliced add of each active input's connected-column row
+    sh.each_active_input(c, [&](int input) {
+        const uint32_t* row = connT + (size_t)input * nw;
         uint32_t x0 = l < nw ? row[l] : 0u;
         uint32_t x1 = (l + 64) < nw ? row[l + 64] : 0u;
 #pragma unroll
-        for (int k = 0; k < HTM_NPLANES; k++) {
+        for (int k = 0; k < NPL; k++) {
             uint32_t t0 = p0[k] & x0, t1 = p1[k] & x1;
             p0[k] ^= x0; p1[k] ^= x1;
             x0 = t0; x1 = t1;
         }
-    }
+    });
     // eligibility: overlap >= stimulusThreshold (bit-sliced compare)
     uint32_t gt0 = 0, gt1 = 0, eq0 = ~0u, eq1 = ~0u;
-    for (int k = HTM_NPLANES - 1; k >= 0; k--) {
+    for (int k = NPL - 1; k >= 0; k--) {
         if ((c.stim_thr >> k) & 1) { eq0 &= p0[k]; eq1 &= p1[k]; }
         else { gt0 |= eq0 & p0[k]; gt1 |= eq1 & p1[k]; eq0 &= ~p0[k]; eq1 &= ~p1[k]; }
     }
@@ -66,7 +99,7 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     uint32_t cand1 = (gt1 | eq1) & ((l + 64) < nw ? ~0u : 0u);
     uint32_t win0 = 0, win1 = 0;
     uint32_t need = (uint32_t)c.num_desired;
-    for (int k = HTM_NPLANES - 1; k >= 0; k--) {
+    for (int k = NPL - 1; k >= 0; k--) {
         uint32_t h0 = cand0 & p0[k], h1 = cand1 & p1[k];
         uint32_t cnt = wave_sum_u32((uint32_t)(__popc(h0) + __popc(h1)));
         if (cnt >= need) {
@@ -98,7 +131,7 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     uint32_t a0 = win0 | keep0, a1 = win1 | keep1;
     uint32_t nz0 = 0, nz1 = 0;
 #pragma unroll
-    for (int k = 0; k < HTM_NPLANES; k++) { nz0 |= p0[k]; nz1 |= p1[k]; }
+    for (int k = 0; k < NPL; k++) { nz0 |= p0[k]; nz1 |= p1[k]; }
     if (l < nw) { sh.act[l] = a0; sh.ovnz[l] = nz0; }
     if (l + 64 < nw) { sh.act[l + 64] = a1; sh.ovnz[l + 64] = nz1; }
     // ascending active list
@@ -118,13 +151,13 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
             if (l < nw) {
                 int32_t v = 0;
 #pragma unroll
-                for (int k = 0; k < HTM_NPLANES; k++) v |= (int32_t)((p0[k] >> bit) & 1u) << k;
+                for (int k = 0; k < NPL; k++) v |= (int32_t)((p0[k] >> bit) & 1u) << k;
                 ov[l * 32 + bit] = v;
             }
             if (l + 64 < nw) {
                 int32_t v = 0;
 #pragma unroll
-                for (int k = 0; k < HTM_NPLANES; k++) v |= (int32_t)((p1[k] >> bit) & 1u) << k;
+                for (int k = 0; k < NPL; k++) v |= (int32_t)((p1[k] >> bit) & 1u) << k;
                 ov[(l + 64) * 32 + bit] = v;
             }
         }
@@ -184,14 +217,21 @@ __device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b
     }
 }
 
-// One SpatialPooler.compute of stream s by the calling workgroup (>= 64
-// threads; learning uses every wave).  sh may live in static or dynamic LDS.
+// SP bookkeeping of one compute (updateBookeepingVars_), by one thread
+template <bool LEARN, class SH>
+__device__ __forceinline__ void sp_count_iteration(const SpBufs& b, int s, SH& sh) {
+    uint32_t* sc = b.scalars + (size_t)s * 4;
+    uint32_t it = sc[0] + 1;
+    sc[0] = it;
+    if (LEARN) sc[1] = sc[1] + 1;
+    sh.iter = it;
+}
+
+// Input stage, encoder: RecordSensor -> MultiEncoder.encodeIntoArray
 template <bool LEARN>
-__device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, const double* values, int s,
-                                             SpShared& sh, int write_overlaps) {
+__device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, const double* values, int s,
+                                              SpShared& sh) {
     const int t = threadIdx.x;
-    const int pw = c.nin_pad >> 5;
-    // ---- encoder (RecordSensor -> MultiEncoder.encodeIntoArray)
     if (t < 64) sh.in[t] = 0;
     if (t == 0) {
         int n = 0;
@@ -201,17 +241,39 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
             for (int k = 0; k < c.enc_w; k++) sh.act_inputs[n++] = f * c.enc_n + bkt + k;
         }
         sh.n_act_inputs = n;
-        uint32_t* sc = b.scalars + (size_t)s * 4;
-        uint32_t it = sc[0] + 1;  // updateBookeepingVars_
-        sc[0] = it;
-        if (LEARN) sc[1] = sc[1] + 1;
-        sh.iter = it;
+        sp_count_iteration<LEARN>(b, s, sh);
     }
     __syncthreads();
     for (int k = t; k < sh.n_act_inputs; k += blockDim.x) {
         int i = sh.act_inputs[k];
         atomicOr(&sh.in[i >> 5], 1u << (i & 31));
     }
+}
+
+// Input stage, external SDR: row s of a [n_streams][nin_pad/32] bitmap (bits
+// past nin are ignored: the link carries exactly inputWidth elements)
+template <bool LEARN>
+__device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int s,
+                                              SpSharedSdr& sh) {
+    const int pw = c.nin_pad >> 5;
+    const uint32_t* row = sdr + (size_t)s * pw;
+    for (int w = threadIdx.x; w < pw; w += blockDim.x) {
+        const int lo = w * 32;
+        uint32_t x = row[w];
+        if (lo + 32 > c.nin) x &= (1u << (c.nin - lo)) - 1u;
+        sh.in[w] = x;
+    }
+    if (threadIdx.x == 0) sp_count_iteration<LEARN>(b, s, sh);
+}
+
+// One SpatialPooler.compute of stream s by the calling workgroup (>= 64
+// threads; learning uses every wave).  sh may live in static or dynamic LDS;
+// `input` is the encoder values (SpShared) or the input SDR (SpSharedSdr).
+template <bool LEARN, class SH, class IN>
+__device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, const IN* input, int s,
+                                             SH& sh, int write_overlaps) {
+    const int t = threadIdx.x;
+    sp_load_input<LEARN>(c, b, input, s, sh);
     __syncthreads();
     if (t < 64) sp_overlap_inhibit(c, b, s, sh, write_overlaps);
     __syncthreads();
@@ -262,6 +324,5 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
             b.scalars[(size_t)s * 4 + 2] = __float_as_uint(c.sp_min_pct_odc * m);
         }
     }
-    (void)pw;
 }
 

@@ -399,21 +399,57 @@ __device__ __forceinline__ void fx_collect_dense(const uint32_t* cnt, uint32_t n
 // the same, and every counter that reaches thr (it happens once: counters
 // only grow) appends base + slot to dst at *qn -- qualification without a
 // sweep over the counters
+// fx_mode bit 0: padding entries skip the atomic (exec-masked) instead of
+// adding into the lane's sink word; bit 1: qualifying segments reserve their
+// list positions with one LDS atomic per wave (ballot ranks) instead of one
+// same-address atomic per lane
 __device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint32_t thr, uint32_t base, int32_t* qn,
-                                                    uint32_t* dst, uint32_t qcap, uint32_t dummy) {
+                                                    uint32_t* dst, uint32_t qcap, uint32_t dummy, int fx_mode) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t old[8];
+    if (fx_mode & 1) {
 #pragma unroll
-    for (int h = 0; h < 8; h++) {  // branch-free: padding goes to the lane's sink word
-        const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        old[h] = atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy + (threadIdx.x & 63)], 1u << ((rel & 3) * 8));
+        for (int h = 0; h < 8; h++) {
+            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+            old[h] = 0u;
+            if (rel != 0xFFFFu) old[h] = atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
+        }
+    } else {
+#pragma unroll
+        for (int h = 0; h < 8; h++) {  // branch-free: padding goes to the lane's sink word
+            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+            old[h] = atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy + (threadIdx.x & 63)], 1u << ((rel & 3) * 8));
+        }
     }
+    if (fx_mode & 2) {
+        uint32_t qmask = 0;
 #pragma unroll
-    for (int h = 0; h < 8; h++) {
-        const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) {
-            const uint32_t i = (uint32_t)atomicAdd(qn, 1);
-            if (i < qcap) dst[i] = base + rel;
+        for (int h = 0; h < 8; h++) {
+            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+            if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) qmask |= 1u << h;
+        }
+        const uint32_t nq = __popc(qmask);
+        const uint32_t tot = wave_sum_u32(nq);
+        if (tot) {  // wave-uniform
+            const uint32_t pre = wave_incl_scan(nq) - nq;
+            uint32_t b0 = 0;
+            if (lane_id() == 0) b0 = (uint32_t)atomicAdd(qn, (int32_t)tot);
+            b0 = __shfl(b0, 0, 64) + pre;
+            for (uint32_t x = qmask; x; x &= x - 1) {
+                const int h = __ffs(x) - 1;
+                const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+                if (b0 < qcap) dst[b0] = base + rel;
+                b0++;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
+            if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) {
+                const uint32_t i = (uint32_t)atomicAdd(qn, 1);
+                if (i < qcap) dst[i] = base + rel;
+            }
         }
     }
 }
@@ -428,7 +464,7 @@ template <bool PUSH>
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
                                           uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy, uint32_t thr = 0,
                                           uint32_t base = 0, int32_t* qn = nullptr, uint32_t* dst = nullptr,
-                                          uint32_t qcap = 0, TmSh* shp = nullptr) {
+                                          uint32_t qcap = 0, TmSh* shp = nullptr, int fx_mode = 0) {
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
         for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
@@ -456,7 +492,7 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
                 STAMP_SH(shp, SB_SLOAD);
             }
 #endif
-            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap, dummy);
+            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap, dummy, fx_mode);
             else fx_count_block(cnt, v[j], dummy);
         }
         STAMP_SH(shp, SB_COUNT);
@@ -624,7 +660,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         if (w < 0) fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, 0, 0, nullptr, nullptr, 0, sh);
         else
             fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, (uint32_t)thr, (uint32_t)w * W, &sh->qn,
-                            t.q1, (uint32_t)c.q_cap, sh);
+                            t.q1, (uint32_t)c.q_cap, sh, c.fx_mode);
         STAMP(t, SB_STREAM);
 #else
         fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, 0, 0, nullptr, nullptr, 0, sh);
@@ -669,10 +705,17 @@ __device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
         // returns.
         const uint32_t slot = t.q1[k];
         const uint2 rec = t.fxrec[slot];
-        t.duty[(size_t)slot * 3 + 1] = rec.y;
-        t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
-        nb += 8u + 8u;
-        emit(k, slot, rec.x, __uint_as_float(rec.y));
+        // the dutyCycle() state write stores the same value every time while
+        // the iteration counter is frozen: only the first one after the index
+        // build changes the record (FX_FRESH marks it done, or never needed)
+        if (!(rec.x & FX_FRESH) || (c.fx_mode & 4)) {  // (fx_mode bit 2: write every time, A/B)
+            t.duty[(size_t)slot * 3 + 1] = rec.y;
+            t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
+            if (!(c.fx_mode & 4)) atomicOr(const_cast<uint32_t*>(&t.fxrec[slot].x), FX_FRESH);
+            nb += 8u;
+        }
+        nb += 8u;
+        emit(k, slot, rec.x & 0xFFFFu, __uint_as_float(rec.y));
     }
     for (uint32_t k = threadIdx.x; k < qn && !fx_pid; k += TM_NT) {
         uint32_t slot = t.q1[k];
@@ -2714,7 +2757,10 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
             uint32_t pos = atomicAdd(&cur[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
             ent[pos] = (uint16_t)(slot - w * W);
         }
-        rec[slot] = make_uint2(meta_cell(m), __float_as_uint(seg_dc_peek(duty, slot, it)));
+        // FX_FRESH: the record already holds what a frozen dutyCycle() stores
+        // (lastDCIter == it past the first tier: age 0 returns without a write)
+        const uint32_t fresh = (it > kDcTier[1] && duty[(size_t)slot * 3 + 2] == it) ? FX_FRESH : 0u;
+        rec[slot] = make_uint2(meta_cell(m) | fresh, __float_as_uint(seg_dc_peek(duty, slot, it)));
         const uint32_t p = pid[slot];
         if (pid_ok && p != ~0u) {
             const uint32_t cm = conn[slot];

@@ -47,9 +47,12 @@ class HTMEngine:
         self.n_columns = cfg.sp_columns
         self.cells_per_column = cfg.tm_cells_per_col
         self.n_cells = cfg.sp_columns * cfg.tm_cells_per_col
+        self.sdr_bits = cfg.sdr_bits        # > 0: the SP reads an input SDR (step_sdr / run_sdr)
+        self.sdr_words = (cfg.sdr_bits + 31) // 32
         self.sp_learn = True
         self.tm_learn = True
-        self.fused = os.environ.get("HTM_FUSED", "1") != "0"  # the engine's default (HTM_OPT_FUSED)
+        # the engine's default (HTM_OPT_FUSED); SDR-input engines always run unfused
+        self.fused = os.environ.get("HTM_FUSED", "1") != "0" and not self.sdr_bits
         self.is_fleet = bool(self._L.htm_is_fleet(self.h))
         if self.is_fleet:
             self.sp_learn = self.tm_learn = False
@@ -136,6 +139,43 @@ class HTMEngine:
             out = torch.empty((T, self.n_streams), dtype=torch.float32, device=v.device)
         check(self._L.htm_run(self.h, T, ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                               self._stream()))
+        return out
+
+    def _sdr(self, sdr) -> torch.Tensor:
+        if not isinstance(sdr, torch.Tensor):
+            sdr = torch.as_tensor(np.ascontiguousarray(np.asarray(sdr, dtype=np.uint32)).view(np.int32))
+        if sdr.dtype not in (torch.int32, torch.uint32):
+            raise TypeError("input SDRs are uint32/int32 word bitmaps [..., n_streams, ceil(sdr_bits/32)]")
+        return sdr.to(device=f"cuda:{self.device}").contiguous()
+
+    def step_sdr(self, sdr, out: torch.Tensor | None = None) -> torch.Tensor:
+        """One network.run(1) of an SDR-fed level (the L2 SPRegion + TMRegion of
+        Models 2/3): sdr is the [N, ceil(sdr_bits/32)] word bitmap the level below
+        produced, e.g. ``l1.get_output("tm_output")`` (bit i of word w = element
+        32*w + i of the L1 TMRegion bottomUpOut).  Returns anomaly scores [N]."""
+        if not self.sdr_bits:
+            raise ValueError("this engine reads encoder values: use step()")
+        x = self._sdr(sdr)
+        if x.numel() != self.n_streams * self.sdr_words:
+            raise ValueError(f"expected {self.n_streams} x {self.sdr_words} words, got {tuple(x.shape)}")
+        if out is None:
+            out = torch.empty(self.n_streams, dtype=torch.float32, device=x.device)
+        check(self._L.htm_step_sdr(self.h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                   self._stream()))
+        return out
+
+    def run_sdr(self, sdr, out: torch.Tensor | None = None) -> torch.Tensor:
+        """sdr [T, N, words] -> scores [T, N]."""
+        if not self.sdr_bits:
+            raise ValueError("this engine reads encoder values: use run()")
+        x = self._sdr(sdr)
+        T = x.shape[0]
+        if x.numel() != T * self.n_streams * self.sdr_words:
+            raise ValueError("sdr must be [T, n_streams, ceil(sdr_bits/32)]")
+        if out is None:
+            out = torch.empty((T, self.n_streams), dtype=torch.float32, device=x.device)
+        check(self._L.htm_run_sdr(self.h, T, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                  self._stream()))
         return out
 
     # --------------------------------------------------------------- outputs
@@ -247,7 +287,7 @@ class HTMEngine:
     def sp_state(self, s: int) -> dict:
         """SP state of stream s in the oracle's dense layout."""
         c = self.config
-        nin = c.n_fields * c.enc_n
+        nin = c.sdr_bits if c.sdr_bits else c.n_fields * c.enc_n
         nin_pad = (nin + 31) // 32 * 32
         nw = c.sp_columns // 32
         pot_words = self.export_state("sp_potmask", self._model_index(s), 1)[0].view(np.uint32).reshape(c.sp_columns, nin_pad // 32)

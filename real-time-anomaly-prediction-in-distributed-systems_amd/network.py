@@ -290,18 +290,26 @@ _IGNORED = {"spVerbosity", "verbosity", "inputWidth", "columnCount", "potentialR
             "temporalImp"}
 
 
-def engine_config(sensor_enc: MultiEncoder, sp_params: dict, tm_params: dict, **engine_opts):
+def engine_config(sensor_enc: MultiEncoder | None, sp_params: dict, tm_params: dict, input_width: int = 0,
+                  **engine_opts):
     """Translate the reference's region parameter dicts into an htm_config
-    (raises ValueError for anything the engine does not implement)."""
-    fields = sensor_enc.fields()
-    if not fields:
-        raise ValueError("the sensor has no encoder (NetworkUtils.createEncoder)")
-    e0 = fields[0]
-    for e in fields[1:]:
-        if (e.n, e.w, e.minval, e.maxval, e.clipInput) != (e0.n, e0.w, e0.minval, e0.maxval, e0.clipInput):
-            raise ValueError("all encoder fields must share n/w/minval/maxval/clipInput")
-    over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_minval=e0.minval, enc_maxval=e0.maxval,
-                enc_clip=int(e0.clipInput))
+    (raises ValueError for anything the engine does not implement).  With
+    sensor_enc None the SP reads an input SDR of input_width bits (a second
+    level, fed the TMRegion bottomUpOut below it: MultiLevelNetworkModel.py:92-94)."""
+    if sensor_enc is not None:
+        fields = sensor_enc.fields()
+        if not fields:
+            raise ValueError("the sensor has no encoder (NetworkUtils.createEncoder)")
+        e0 = fields[0]
+        for e in fields[1:]:
+            if (e.n, e.w, e.minval, e.maxval, e.clipInput) != (e0.n, e0.w, e0.minval, e0.maxval, e0.clipInput):
+                raise ValueError("all encoder fields must share n/w/minval/maxval/clipInput")
+        over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_minval=e0.minval, enc_maxval=e0.maxval,
+                    enc_clip=int(e0.clipInput))
+        width = sensor_enc.getWidth()
+    else:
+        over = dict(sdr_bits=int(input_width))
+        width = int(input_width)
     for params, mapping, fixed, region in ((sp_params, _SP_MAP, _SP_FIXED, "SPRegion"),
                                            (tm_params, _TM_MAP, _TM_FIXED, "TMRegion")):
         for k, v in params.items():
@@ -312,9 +320,8 @@ def engine_config(sensor_enc: MultiEncoder, sp_params: dict, tm_params: dict, **
                     raise ValueError("%s %s=%r is not supported (only %r)" % (region, k, v, fixed[k]))
             elif k not in _IGNORED:
                 raise ValueError("%s parameter %r is not supported" % (region, k))
-    width = sensor_enc.getWidth()
     if int(sp_params.get("inputWidth", 0) or width) != width:
-        raise ValueError("SPRegion inputWidth %s != encoder width %d" % (sp_params.get("inputWidth"), width))
+        raise ValueError("SPRegion inputWidth %s != the width of its input (%d)" % (sp_params.get("inputWidth"), width))
     cols = int(sp_params.get("columnCount", 2048))
     if int(tm_params.get("columnCount", cols)) != cols or int(tm_params.get("inputWidth", cols)) != cols:
         raise ValueError("TMRegion columnCount/inputWidth must equal the SP columnCount")
@@ -322,9 +329,30 @@ def engine_config(sensor_enc: MultiEncoder, sp_params: dict, tm_params: dict, **
     return _lib.default_config(**over)
 
 
+class _Level:
+    """One SPRegion -> TMRegion level of the graph and the engine that runs it
+    for every stream (level 0 reads the sensor, level k > 0 the bottomUpOut of
+    level k - 1)."""
+
+    def __init__(self, sp: Region, tm: Region):
+        self.sp, self.tm = sp, tm
+        self.engine = None
+        self.scores = None
+
+
 class Network:
     """Batched nupic.engine.Network: `Network()` builds an empty graph,
-    `Network(path)` loads a saved one (ModelTesting.py:176)."""
+    `Network(path)` loads a saved one (ModelTesting.py:176).
+
+    Graphs: RecordSensor -> SPRegion -> TMRegion, optionally followed by more
+    SPRegion -> TMRegion levels each fed the TMRegion bottomUpOut below it (the
+    two-level Models 2/3, MultiLevelNetworkModel.py:53-127,
+    MultiLevelNetworkAnomaly.py:61-127), and SDRClassifierRegions fed any
+    level's TMRegion bottomUpOut.  The Model-2 feedback link (L2 TMRegion
+    topDownOut -> L1 SPRegion topDownIn, MultiLevelNetworkModel.py:113-114) is
+    accepted and has no effect: an SPRegion reads topDownIn only in topDownMode,
+    which NetworkUtils never enables for an SPRegion (NetworkUtils.py:126-136),
+    so the reference's bottom-up results do not depend on it either."""
 
     def __init__(self, path: str | None = None, n_streams: int = 1, device: int | None = None, **engine_opts):
         self.regions = {}
@@ -332,15 +360,20 @@ class Network:
         self.n_streams = int(n_streams)
         self.device = device
         self.engine_opts = dict(engine_opts)
-        self.engine = None
-        self._scores = None
+        self.levels: list[_Level] = []
+        self._cls_level = {}  # classifier region name -> level index
         self._learn_dirty = False
         if path is not None:
             self._load(path)
 
+    @property
+    def engine(self):
+        """The first level's engine (the only one of a Model-1 graph)."""
+        return self.levels[0].engine if self.levels else None
+
     # ------------------------------------------------------------ building
     def addRegion(self, name, nodeType, nodeParams="{}"):
-        if self.engine is not None:
+        if self.levels:
             raise RuntimeError("cannot add regions after the network is initialized")
         if name in self.regions:
             raise ValueError("region %r already exists" % name)
@@ -365,19 +398,44 @@ class Network:
             raise RuntimeError("the engine runs exactly one %s per network (found %d)" % (kind, len(rs)))
         return rs[0]
 
-    def _check_graph(self):
-        sensor, sp, tm = self._find(SENSOR), self._find(SP), self._find(TM)
-        feed = {(s, d) for s, d, so, di in self.links if so == "bottomUpOut" or (so == "dataOut")}
-        feed |= {(s, d) for s, d, so, di in self.links if di == "bottomUpIn"}
-        if (sensor.name, sp.name) not in feed or (sp.name, tm.name) not in feed:
-            raise RuntimeError("the graph must link sensor -> SPRegion -> TMRegion (NetworkModel.py:61,67)")
-        return sensor, sp, tm
+    def _feed(self):
+        """bottom-up links (src, dest): bottomUpOut/dataOut -> bottomUpIn"""
+        return {(s, d) for s, d, so, di in self.links if di == "bottomUpIn" or so in ("bottomUpOut", "dataOut")}
 
-    def initialize(self):
-        if self.engine is not None:
-            return
-        from .engine import HTMEngine
-        sensor, sp, tm = self._check_graph()
+    def _chain(self):
+        """The sensor and its SPRegion -> TMRegion levels in bottom-up order."""
+        sensor = self._find(SENSOR)
+        feed = self._feed()
+        levels, src = [], sensor.name
+        while True:
+            sps = [r for r in self.regions.values() if r.type == SP and (src, r.name) in feed]
+            if not sps:
+                break
+            if len(sps) > 1:
+                raise RuntimeError("%s feeds %d SPRegions; the engine runs one chain" % (src, len(sps)))
+            tms = [r for r in self.regions.values() if r.type == TM and (sps[0].name, r.name) in feed]
+            if len(tms) != 1:
+                raise RuntimeError("SPRegion %s must feed exactly one TMRegion (NetworkModel.py:67)" % sps[0].name)
+            if any(lv.sp is sps[0] for lv in levels):
+                raise RuntimeError("the SPRegion -> TMRegion chain has a cycle")
+            levels.append(_Level(sps[0], tms[0]))
+            src = tms[0].name
+        if not levels:
+            raise RuntimeError("the graph must link sensor -> SPRegion -> TMRegion (NetworkModel.py:61,67)")
+        on_chain = {lv.sp.name for lv in levels} | {lv.tm.name for lv in levels}
+        for r in self.regions.values():
+            if r.type in (SP, TM) and r.name not in on_chain:
+                raise RuntimeError("region %s is not on the sensor -> SPRegion -> TMRegion chain" % r.name)
+        cls_level = {}
+        for r in self.regions.values():
+            if r.type == CLASSIFIER:
+                src_lv = [k for k, lv in enumerate(levels) if (lv.tm.name, r.name) in feed]
+                if len(src_lv) != 1:
+                    raise RuntimeError("SDRClassifierRegion %s must be fed one TMRegion bottomUpOut" % r.name)
+                cls_level[r.name] = src_lv[0]
+        return sensor, levels, cls_level
+
+    def _sensor_encoder(self, sensor):
         enc = sensor.getSelf().encoder
         if enc is None:
             raise RuntimeError("sensor %r has no encoder" % sensor.name)
@@ -385,93 +443,118 @@ class Network:
             m = MultiEncoder()
             m.addEncoder(enc.name, enc)
             enc = m
-        cfg = engine_config(enc, sp.getSelf().params, tm.getSelf().params, **self.engine_opts)
-        self.engine = HTMEngine(self.n_streams, config=cfg, device=self.device)
-        self._init_classifier()
+        return enc
+
+    def initialize(self):
+        if self.levels:
+            return
+        from .engine import HTMEngine
+        sensor, levels, cls_level = self._chain()
+        enc = self._sensor_encoder(sensor)
+        try:
+            for k, lv in enumerate(levels):
+                if k == 0:
+                    cfg = engine_config(enc, lv.sp.getSelf().params, lv.tm.getSelf().params, **self.engine_opts)
+                else:
+                    width = levels[k - 1].engine.n_cells  # TMRegion bottomUpOut element count
+                    cfg = engine_config(None, lv.sp.getSelf().params, lv.tm.getSelf().params, input_width=width,
+                                        **self.engine_opts)
+                lv.engine = HTMEngine(self.n_streams, config=cfg, device=self.device)
+        except Exception:
+            for lv in levels:
+                if lv.engine is not None:
+                    lv.engine.close()
+            raise
+        self.levels, self._cls_level = levels, cls_level
+        for name in cls_level:
+            self._init_classifier(self.regions[name])
         self._learning_changed()
 
-    def _classifier_region(self):
-        rs = [r for r in self.regions.values() if r.type == CLASSIFIER]
-        if len(rs) > 1:
-            raise RuntimeError("the engine runs at most one SDRClassifierRegion per network")
-        return rs[0] if rs else None
+    def _level_of(self, region):
+        for lv in self.levels:
+            if region is lv.sp or region is lv.tm:
+                return lv
+        raise RuntimeError("region %s is not on the engine's chain" % region.name)
 
-    def _init_classifier(self, cls_obj=None):
-        from .classifier import SDRClassifier
-        r = self._classifier_region()
-        if r is None:
-            return
-        impl = r.getSelf()
+    def _first_field(self):
         enc = self._find(SENSOR).getSelf().encoder
-        f0 = enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
+        return enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
+
+    def _init_classifier(self, r, cls_obj=None):
+        from .classifier import SDRClassifier
+        impl = r.getSelf()
+        f0 = self._first_field()
         nb = f0.n - f0.w + 1  # ScalarEncoder buckets (clipped, non-periodic)
         if impl.maxCategoryCount < nb:
             raise ValueError("maxCategoryCount %d < %d encoder buckets" % (impl.maxCategoryCount, nb))
+        eng = self.levels[self._cls_level[r.name]].engine
         impl.classifier = cls_obj if cls_obj is not None else SDRClassifier(
-            self.n_streams, self.engine.n_cells, nb, steps=impl.stepsList, alpha=impl.alpha,
-            device=self.engine.device)
+            self.n_streams, eng.n_cells, nb, steps=impl.stepsList, alpha=impl.alpha, device=eng.device)
         impl.actualValues = np.zeros((self.n_streams, impl.maxCategoryCount))
         impl.probabilities = np.zeros((self.n_streams, len(impl.stepsList) * impl.maxCategoryCount))
 
-    def _run_classifier(self, vals):
-        """SDRClassifierRegion.compute of every stream after the TM step: TM
-        bottomUpOut, bucketIdxOut / actValueOut of the first field (a missing
-        value does not learn)."""
-        r = self._classifier_region()
-        if r is None:
-            return
-        impl = r.getSelf()
-        learn, infer = r.modes["learningMode"], r.modes["inferenceMode"]
-        enc = self._find(SENSOR).getSelf().encoder
-        f0 = enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
-        pat = self.engine.get_output("tm_output")
-        bucket = f0.bucket_indices(vals[:, 0]) if learn else None
-        prob, act = impl.classifier.compute(pat, bucket, vals[:, 0] if learn else None, learn=learn, infer=infer)
-        impl.classifier.status()  # raises like NuPIC on an empty pattern (this record only)
-        impl.recordNum += 1
-        if infer:
-            nb, n = impl.classifier.n_buckets, impl.maxCategoryCount
-            impl.actualValues[:, :nb] = act.cpu().numpy()
-            p = prob.cpu().numpy()
-            for i in range(len(impl.stepsList)):
-                impl.probabilities[:, i * n:i * n + nb] = p[:, i]
+    def _run_classifiers(self, vals):
+        """SDRClassifierRegion.compute of every stream after the TM steps: its
+        level's TM bottomUpOut, bucketIdxOut / actValueOut of the first encoder
+        field (a missing value does not learn)."""
+        f0 = None
+        for name, k in self._cls_level.items():
+            r = self.regions[name]
+            impl = r.getSelf()
+            learn, infer = r.modes["learningMode"], r.modes["inferenceMode"]
+            f0 = f0 or self._first_field()
+            pat = self.levels[k].engine.get_output("tm_output")
+            bucket = f0.bucket_indices(vals[:, 0]) if learn else None
+            prob, act = impl.classifier.compute(pat, bucket, vals[:, 0] if learn else None, learn=learn, infer=infer)
+            impl.classifier.status()  # raises like NuPIC on an empty pattern (this record only)
+            impl.recordNum += 1
+            if infer:
+                nb, n = impl.classifier.n_buckets, impl.maxCategoryCount
+                impl.actualValues[:, :nb] = act.cpu().numpy()
+                p = prob.cpu().numpy()
+                for i in range(len(impl.stepsList)):
+                    impl.probabilities[:, i * n:i * n + nb] = p[:, i]
 
     def _learning_changed(self):
         self._learn_dirty = True
 
     def _apply_learning(self):
-        if self._learn_dirty and self.engine is not None:
-            sp, tm = self._find(SP), self._find(TM)
-            self.engine.set_learning(sp.modes["learningMode"], tm.modes["learningMode"])
+        if self._learn_dirty and self.levels:
+            for lv in self.levels:
+                lv.engine.set_learning(lv.sp.modes["learningMode"], lv.tm.modes["learningMode"])
             self._learn_dirty = False
 
     # ------------------------------------------------------------- running
     def run(self, n):
         """network.run(n): n lockstep steps of every stream (NetworkModel.py:127).
         Each step pulls one record (a value per stream and field) from the
-        sensor's data source, like RecordSensor.compute does."""
+        sensor's data source, like RecordSensor.compute does, and runs the
+        levels bottom-up (the links carry no delay)."""
         self.initialize()
         self._apply_learning()
         import torch
         sensor = self._find(SENSOR).getSelf()
         if sensor.dataSource is None:
             raise RuntimeError("sensor has no dataSource")
+        l0 = self.levels[0]
         for _ in range(int(n)):
             vals = np.asarray(sensor.dataSource.getNextRecord(), dtype=np.float64)
-            if vals.shape != (self.n_streams, self.engine.n_fields):
+            if vals.shape != (self.n_streams, l0.engine.n_fields):
                 raise ValueError("record shape %s != (%d streams, %d fields)" %
-                                 (vals.shape, self.n_streams, self.engine.n_fields))
+                                 (vals.shape, self.n_streams, l0.engine.n_fields))
             sensor.values = vals
-            self._scores = self.engine.step(torch.from_numpy(np.ascontiguousarray(vals).ravel()))
-            self._run_classifier(vals)
+            l0.scores = l0.engine.step(torch.from_numpy(np.ascontiguousarray(vals).ravel()))
+            for below, lv in zip(self.levels, self.levels[1:]):
+                lv.scores = lv.engine.step_sdr(below.engine.get_output("tm_output"))
+            self._run_classifiers(vals)
         # NuPIC raises (NTA_THROW) when a Cells4 pool limit is hit; the engine
         # records the overflow per stream -- surface it the same way
-        self.engine.status()
+        for lv in self.levels:
+            lv.engine.status()
 
     def _output(self, region, name):
-        if self.engine is None:
+        if not self.levels:
             raise RuntimeError("network has not run yet")
-        eng = self.engine
         if region.type == SENSOR:
             vals = region.getSelf().values
             if vals is None:
@@ -479,19 +562,22 @@ class Network:
             if name == "actValueOut":
                 return vals[:, 0].astype(np.float64)
             if name == "bucketIdxOut":
-                enc = region.getSelf().encoder
-                e = enc.fields()[0] if isinstance(enc, MultiEncoder) else enc
-                return e.bucket_indices(vals[:, 0]).astype(np.float64)
+                return self._first_field().bucket_indices(vals[:, 0]).astype(np.float64)
             if name == "sourceOut":
                 return vals.copy()
         elif region.type == SP:
+            eng = self._level_of(region).engine
             if name == "bottomUpOut":
                 return eng.get_output("active_columns").cpu().numpy().astype(np.float32)
         elif region.type == TM:
+            lv = self._level_of(region)
+            eng = lv.engine
             if name == "anomalyScore":
                 if not region.modes["anomalyMode"]:
                     raise RuntimeError("anomalyScore needs anomalyMode True (NetworkUtils.py:152)")
-                return self._scores.cpu().numpy()
+                if lv.scores is None:
+                    raise RuntimeError("network has not run yet")
+                return lv.scores.cpu().numpy()
             if name == "bottomUpOut":
                 return eng.bitmap_to_dense(eng.get_output("tm_output")).astype(np.float32)
             if name == "topDownOut":
@@ -516,18 +602,30 @@ class Network:
                 return one(out)
         raise ValueError("region %s (%s) has no output %r" % (region.name, region.type, name))
 
-    def scores_tensor(self):
-        """Device tensor of the last step's anomaly scores (no host copy)."""
-        return self._scores
+    def scores_tensor(self, level: int = -1):
+        """Device tensor of the last step's anomaly scores of a level (default:
+        the top one, whose TMRegion anomalyScore the two-level models report,
+        MultiLevelNetworkModel.py:150) -- no host copy."""
+        return self.levels[level].scores if self.levels else None
 
     # ----------------------------------------------------------- save/load
+    @staticmethod
+    def _engine_file(k):
+        return _ENGINE_FILE if k == 0 else "engine_l%d.htm" % (k + 1)
+
+    @staticmethod
+    def _cls_file(name, first):
+        return _CLS_FILE if first else "classifier_%s.npz" % name
+
     def save(self, path):
         """network.save(path) (NetworkUtils.py:156-159): a bundle directory like
         NuPIC's .nta -- network.json (regions, parameters, links, modes) plus
-        engine.htm (every stream's SP/TM state, htm_save)."""
+        one engine file per level (every stream's SP/TM state, htm_save:
+        engine.htm, engine_l2.htm, ...) and the classifiers' state."""
         self.initialize()
         self._apply_learning()
-        self.engine.status()  # never save a state whose pools overflowed
+        for lv in self.levels:
+            lv.engine.status()  # never save a state whose pools overflowed
         os.makedirs(path, exist_ok=True)
         meta = {"n_streams": self.n_streams, "links": self.links, "regions": []}
         for r in self.regions.values():
@@ -541,10 +639,10 @@ class Network:
             meta["regions"].append(ent)
         with open(os.path.join(path, _META_FILE), "w") as f:
             json.dump(meta, f, indent=1)
-        self.engine.save(os.path.join(path, _ENGINE_FILE))
-        cr = self._classifier_region()
-        if cr is not None:
-            cr.getSelf().classifier.save(os.path.join(path, _CLS_FILE))
+        for k, lv in enumerate(self.levels):
+            lv.engine.save(os.path.join(path, self._engine_file(k)))
+        for i, name in enumerate(self._cls_level):
+            self.regions[name].getSelf().classifier.save(os.path.join(path, self._cls_file(name, i == 0)))
         return path
 
     def _load(self, path):
@@ -564,13 +662,23 @@ class Network:
                 r.getSelf().encoder = enc
                 r.getSelf().predictedField = ent.get("predictedField")
         self.links = [tuple(x) for x in meta["links"]]
-        self.engine = HTMEngine.load(os.path.join(path, _ENGINE_FILE), device=self.device)
-        if self.engine.n_streams != self.n_streams:
-            raise RuntimeError("engine file holds %d streams, network.json says %d" %
-                               (self.engine.n_streams, self.n_streams))
+        _, levels, cls_level = self._chain()
+        try:
+            for k, lv in enumerate(levels):
+                lv.engine = HTMEngine.load(os.path.join(path, self._engine_file(k)), device=self.device)
+                if lv.engine.n_streams != self.n_streams:
+                    raise RuntimeError("engine file holds %d streams, network.json says %d" %
+                                       (lv.engine.n_streams, self.n_streams))
+        except Exception:
+            for lv in levels:
+                if lv.engine is not None:
+                    lv.engine.close()
+            raise
+        self.levels, self._cls_level = levels, cls_level
         self._learn_dirty = True
-        cr = self._classifier_region()
-        if cr is not None:
-            from .classifier import SDRClassifier
-            cp = os.path.join(path, _CLS_FILE)
-            self._init_classifier(SDRClassifier.load(cp, device=self.engine.device) if os.path.exists(cp) else None)
+        from .classifier import SDRClassifier
+        for i, name in enumerate(cls_level):
+            cp = os.path.join(path, self._cls_file(name, i == 0))
+            eng = self.levels[cls_level[name]].engine
+            self._init_classifier(self.regions[name],
+                                  SDRClassifier.load(cp, device=eng.device) if os.path.exists(cp) else None)

@@ -92,6 +92,34 @@ def test_graph_errors_are_raised_before_any_gpu_work(rt):
         net.run(1)  # no SP/TM regions
 
 
+def test_second_level_config_reads_the_l1_bottom_up_out(rt):
+    # MultiLevelNetworkModel.py:92-93: l2 inputWidth = L1 TMRegion bottomUpOut count
+    cfg = rt.network.engine_config(None, dict(ref.SP_PARAMS, inputWidth=24576), ref.TM_PARAMS, input_width=24576)
+    d = cfg.as_dict()
+    assert d["sdr_bits"] == 24576 and d["sp_columns"] == 2048 and d["tm_cells_per_col"] == 12
+    with pytest.raises(ValueError):
+        rt.network.engine_config(None, dict(ref.SP_PARAMS, inputWidth=2048), ref.TM_PARAMS, input_width=24576)
+
+
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_multilevel_graph_resolves_to_two_levels(rt, anomaly):
+    """The Model 2/3 graphs (feedback link included) resolve to a sensor and two
+    SP -> TM levels; classifiers attach to the level that feeds them."""
+    net = ref.create_multilevel_network(rt, rt.BatchRecordStream(["cpu", "mem"] if anomaly else ["cpu"]),
+                                        anomaly=anomaly)
+    sensor, levels, cls = net._chain()
+    assert sensor.name == ref.SENSOR
+    assert [(lv.sp.name, lv.tm.name) for lv in levels] == [(ref.SPR, ref.TMR), (ref.L2_SPR, ref.L2_TMR)]
+    assert cls == ({ref.CLS: 0, ref.L2_CLS: 1} if anomaly else {ref.L2_CLS: 1})
+
+
+def test_dangling_second_level_raises(rt):
+    net = ref.create_one_level_network(rt, rt.BatchRecordStream(["cpu"]))
+    net.addRegion("l2sp", "py.SPRegion", "{}")  # never linked
+    with pytest.raises(RuntimeError, match="not on the"):
+        net._chain()
+
+
 @pytest.mark.gpu
 def test_model1_through_the_facade_matches_golden(rt, traces, tmp_path):
     """ModelTraining/ModelTesting's call pattern through the drop-in surface:
@@ -156,3 +184,52 @@ def test_batched_facade_streams_are_independent(rt, traces):
         a = net.regions[ref.TMR].getOutputData("anomalyScore")
         assert a.shape == (n,)
         assert a[2] == one.regions[ref.TMR].getOutputData("anomalyScore")[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("anomaly", [False, True])
+def test_multilevel_facade_matches_engine_pair_and_reloads(rt, traces, tmp_path, anomaly):
+    """Models 2/3 through the drop-in surface: the l2 TMRegion anomalyScore
+    (MultiLevelNetworkModel.py:150, MultiLevelNetworkAnomaly.py:171) equals two
+    engines driven directly (L1 step -> tm_output -> L2 step_sdr, whose oracle
+    parity tests/test_multilevel_gpu.py holds), and a saved bundle
+    (network2/3.nta: engine.htm + engine_l2.htm + classifiers) resumes exactly."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    names = ["cpu", "mem"] if anomaly else ["cpu"]
+    ds = rt.BatchRecordStream(names)
+    net = ref.create_multilevel_network(rt, ds, anomaly=anomaly, seg_capacity=1 << 13)
+    nf = len(names)
+    l1 = rt.HTMEngine(1, n_fields=nf, seg_capacity=1 << 13)
+    l2 = rt.HTMEngine(1, sdr_bits=24576, seg_capacity=1 << 13)
+    cpu = np.asarray(traces["train"][:90], np.float64)
+    mem = np.clip(100.0 - cpu, 0, 100)
+    recs = np.stack([cpu, mem], axis=1)[:, :nf]
+    tmr2 = net.regions[ref.L2_TMR]
+    for k in range(60):
+        ds.setData(*[float(x) for x in recs[k]])
+        net.run(1)
+        l1.step(torch.tensor(recs[k], device="cuda"))
+        want = l2.step_sdr(l1.get_output("tm_output")).cpu().numpy()[0]
+        assert tmr2.getOutputData("anomalyScore")[0] == want, f"step {k}"
+    assert net.regions[ref.L2_SPR].getOutputData("bottomUpOut").shape == (1, 2048)
+    p = net.regions[ref.L2_CLS].getOutputData("probabilities")
+    assert p.shape == (7 * 1000,) and np.allclose(p.reshape(7, 1000).sum(axis=1), 1.0)
+    path = net.save(str(tmp_path / ("network3.nta" if anomaly else "network2.nta")))
+    assert os.path.exists(os.path.join(path, "engine_l2.htm"))
+    net2 = rt.Network(path)
+    ds2 = rt.BatchRecordStream(names)
+    net2.regions[ref.SENSOR].dataSource = ds2
+    for r in (net, net2):
+        r.regions[ref.TMR].setParameter("learningMode", False)
+        r.regions[ref.L2_TMR].setParameter("learningMode", False)
+    for k in range(60, 90):
+        for d in (ds, ds2):
+            d.setData(*[float(x) for x in recs[k]])
+        net.run(1)
+        net2.run(1)
+        a = net.regions[ref.L2_TMR].getOutputData("anomalyScore")[0]
+        assert a == net2.regions[ref.L2_TMR].getOutputData("anomalyScore")[0], f"step {k}"
+        assert np.array_equal(net.regions[ref.L2_CLS].getOutputData("probabilities"),
+                              net2.regions[ref.L2_CLS].getOutputData("probabilities"))
