@@ -101,6 +101,13 @@ typedef struct {
      * MultiLevelNetworkAnomaly.py:112-116); steps go through htm_step_sdr /
      * htm_run_sdr.  <= 32768 */
     int32_t sdr_bits;
+    /* Per-field encoder range: field f uses [field_minval[f], field_maxval[f]]
+     * when field_maxval[f] > field_minval[f], else [enc_minval, enc_maxval] --
+     * the 4-field aggregate of StreamAggregator.py:101-115 (cpu %, mem %, mean
+     * and max response time) does not share one range.  n, w and clipInput
+     * stay shared.  Zero (htm_default_config) = the shared range. */
+    double field_minval[4];
+    double field_maxval[4];
 } htm_config;
 
 typedef struct htm_engine htm_engine;

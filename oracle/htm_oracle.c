@@ -108,21 +108,24 @@ static void rng_sample(rng_t* g, const uint32_t* pop, uint32_t n, uint32_t* out,
  * in sorted name order by MultiEncoder (NetworkUtils.py:77-108).
  * ===================================================================== */
 /* returns the first on-bit (bucket index) or -1 for a missing value */
-static int enc_first_on_bit(const orc_params* p, double x) {
+static int enc_first_on_bit(const orc_params* p, int f, double x) {
     if (isnan(x)) return -1; /* SENTINEL_VALUE_FOR_MISSING_DATA -> all zeros */
-    double rangeInternal = p->enc_maxval - p->enc_minval;
+    const int own = p->field_maxval[f] > p->field_minval[f];
+    const double minval = own ? p->field_minval[f] : p->enc_minval;
+    const double maxval = own ? p->field_maxval[f] : p->enc_maxval;
+    double rangeInternal = maxval - minval;
     double resolution = rangeInternal / (double)(p->enc_n - p->enc_w);
     int halfwidth = (p->enc_w - 1) / 2;
     int padding = halfwidth;
-    if (x < p->enc_minval) {
+    if (x < minval) {
         if (!p->enc_clip) return -1;
-        x = p->enc_minval;
+        x = minval;
     }
-    if (x > p->enc_maxval) {
+    if (x > maxval) {
         if (!p->enc_clip) return -1;
-        x = p->enc_maxval;
+        x = maxval;
     }
-    int centerbin = (int)(((x - p->enc_minval) + resolution / 2.0) / resolution) + padding;
+    int centerbin = (int)(((x - minval) + resolution / 2.0) / resolution) + padding;
     return centerbin - halfwidth;
 }
 
@@ -130,7 +133,7 @@ static void enc_encode(const orc_params* p, const double* values, uint8_t* out) 
     int nin = p->n_fields * p->enc_n;
     memset(out, 0, (size_t)nin);
     for (int f = 0; f < p->n_fields; f++) {
-        int b = enc_first_on_bit(p, values[f]);
+        int b = enc_first_on_bit(p, f, values[f]);
         if (b < 0) continue;
         for (int k = 0; k < p->enc_w; k++) out[f * p->enc_n + b + k] = 1;
     }

@@ -73,6 +73,12 @@ typedef struct {
      * fed a TM's bottomUpOut, MultiLevelNetworkModel.py:92-94); the encoder is
      * unused and steps go through orc_step_sdr */
     int32_t sdr_bits;
+    /* per-field ScalarEncoder range (the aggregate's cpu %, mem %, mean and max
+     * response time, StreamAggregator.py:101-115): field f uses
+     * [field_minval[f], field_maxval[f]] when field_maxval[f] > field_minval[f],
+     * else [enc_minval, enc_maxval] */
+    double field_minval[4];
+    double field_maxval[4];
 } orc_params;
 
 #define ORC_VAR_SP_TIE_LOW       0x001u /* global inhibition: ties -> LOWER index (strict '>' admission) */

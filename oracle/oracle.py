@@ -37,6 +37,7 @@ class OrcParams(ctypes.Structure):
         ("tm_max_lrn_backtrack", ctypes.c_int32), ("tm_max_seq_length", ctypes.c_int32),
         ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
         ("variant", ctypes.c_uint32), ("sdr_bits", ctypes.c_int32),
+        ("field_minval", ctypes.c_double * 4), ("field_maxval", ctypes.c_double * 4),
     ]
 
 

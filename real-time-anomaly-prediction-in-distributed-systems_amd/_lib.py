@@ -63,10 +63,12 @@ class HtmConfig(ctypes.Structure):
         ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
         ("seg_capacity", ctypes.c_int32), ("upd_capacity", ctypes.c_int32), ("seed_stride", ctypes.c_int32),
         ("sdr_bits", ctypes.c_int32),
+        ("field_minval", ctypes.c_double * 4), ("field_maxval", ctypes.c_double * 4),
     ]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: (list(v) if isinstance(v, ctypes.Array) else v)
+                for k, v in ((k, getattr(self, k)) for k, _ in self._fields_)}
 
 
 class TmHeader(ctypes.Structure):

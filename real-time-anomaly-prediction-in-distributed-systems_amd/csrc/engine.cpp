@@ -167,9 +167,12 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.enc_n = c.enc_n;
     d.enc_w = c.enc_w;
     d.enc_clip = c.enc_clip;
-    d.enc_min = c.enc_minval;
-    d.enc_max = c.enc_maxval;
-    d.enc_resolution = (c.enc_maxval - c.enc_minval) / (double)(c.enc_n - c.enc_w);
+    for (int f = 0; f < 4; f++) {
+        const bool own = c.field_maxval[f] > c.field_minval[f];
+        d.enc_min[f] = own ? c.field_minval[f] : c.enc_minval;
+        d.enc_max[f] = own ? c.field_maxval[f] : c.enc_maxval;
+        d.enc_resolution[f] = (d.enc_max[f] - d.enc_min[f]) / (double)(c.enc_n - c.enc_w);
+    }
     d.enc_halfwidth = (c.enc_w - 1) / 2;
     d.nin = sdr ? c.sdr_bits : c.n_fields * c.enc_n;
     d.sdr_in = sdr ? 1 : 0;
@@ -262,6 +265,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.fx_win = (int32_t)win;
     d.fx_nwin = (int32_t)((d.seg_cap + d.fx_win - 1) / d.fx_win);
     d.fx_pcap = d.fx_win < 65535 ? d.fx_win : 65535;
+    if (const char* env = std::getenv("HTM_FX_PID"))  // A/B knob: 0 = no pid lists (rows path)
+        if (std::atoi(env) == 0) d.fx_pcap = 0;
     d.fx_noff = d.ncells * d.fx_nwin + d.ncells + 1;
     return HTM_OK;
 }

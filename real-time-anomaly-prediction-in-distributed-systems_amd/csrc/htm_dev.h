@@ -37,7 +37,7 @@
 struct DevCfg {
     // encoder
     int32_t n_fields, enc_n, enc_w, enc_clip;
-    double enc_min, enc_max, enc_resolution;
+    double enc_min[4], enc_max[4], enc_resolution[4];  // per field
     int32_t enc_halfwidth;
     // SP
     int32_t nin, nin_pad, ncol, nw;      // nw = ncol/32

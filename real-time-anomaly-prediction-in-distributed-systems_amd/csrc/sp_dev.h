@@ -6,17 +6,18 @@
 #include "htm_dev.h"
 
 // ScalarEncoder._getFirstOnBit (double arithmetic, NaN -> missing)
-__device__ __forceinline__ int enc_first_on_bit(const DevCfg& c, double x) {
+__device__ __forceinline__ int enc_first_on_bit(const DevCfg& c, int f, double x) {
     if (isnan(x)) return -1;
-    if (x < c.enc_min) {
+    const double lo = c.enc_min[f], hi = c.enc_max[f], res = c.enc_resolution[f];
+    if (x < lo) {
         if (!c.enc_clip) return -1;
-        x = c.enc_min;
+        x = lo;
     }
-    if (x > c.enc_max) {
+    if (x > hi) {
         if (!c.enc_clip) return -1;
-        x = c.enc_max;
+        x = hi;
     }
-    double q = __ddiv_rn(__dadd_rn(__dadd_rn(x, -c.enc_min), __ddiv_rn(c.enc_resolution, 2.0)), c.enc_resolution);
+    double q = __ddiv_rn(__dadd_rn(__dadd_rn(x, -lo), __ddiv_rn(res, 2.0)), res);
     int centerbin = (int)q + c.enc_halfwidth;
     return centerbin - c.enc_halfwidth;
 }
@@ -236,7 +237,7 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
     if (t == 0) {
         int n = 0;
         for (int f = 0; f < c.n_fields; f++) {
-            int bkt = enc_first_on_bit(c, values[(size_t)s * c.n_fields + f]);
+            int bkt = enc_first_on_bit(c, f, values[(size_t)s * c.n_fields + f]);
             if (bkt < 0) continue;
             for (int k = 0; k < c.enc_w; k++) sh.act_inputs[n++] = f * c.enc_n + bkt + k;
         }

@@ -301,11 +301,18 @@ def engine_config(sensor_enc: MultiEncoder | None, sp_params: dict, tm_params: d
         if not fields:
             raise ValueError("the sensor has no encoder (NetworkUtils.createEncoder)")
         e0 = fields[0]
+        if len(fields) > 4:
+            raise ValueError("at most 4 encoder fields (got %d)" % len(fields))
         for e in fields[1:]:
-            if (e.n, e.w, e.minval, e.maxval, e.clipInput) != (e0.n, e0.w, e0.minval, e0.maxval, e0.clipInput):
-                raise ValueError("all encoder fields must share n/w/minval/maxval/clipInput")
+            if (e.n, e.w, e.clipInput) != (e0.n, e0.w, e0.clipInput):
+                raise ValueError("all encoder fields must share n/w/clipInput")
         over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_minval=e0.minval, enc_maxval=e0.maxval,
                     enc_clip=int(e0.clipInput))
+        if any((e.minval, e.maxval) != (e0.minval, e0.maxval) for e in fields[1:]):
+            # per-field ranges (e.g. cpu/mem % next to response times in ms)
+            pad = [0.0] * (4 - len(fields))
+            over["field_minval"] = tuple([float(e.minval) for e in fields] + pad)
+            over["field_maxval"] = tuple([float(e.maxval) for e in fields] + pad)
         width = sensor_enc.getWidth()
     else:
         over = dict(sdr_bits=int(input_width))

@@ -1,0 +1,146 @@
+"""BASELINE.json configs 3, 4 and 5 at (or near) their stated sizes, against
+independent oracle models on sampled streams, plus the size-independent
+properties the domain offers (identical inputs -> identical outputs; a stream
+is unaffected by the other streams of its launch).
+
+Config 3: 65,536 streams learning on (BASELINE configs[2]) -- here 512 fresh
+          streams with per-stream seeds, every step of 8 sampled streams
+          checked against the oracle and the full SP/TM state of two.
+Config 4: fleet mode, 131,072 streams sharing one frozen model (configs[3]).
+Config 5: the cpu / mem / mean / max response-time aggregate
+          (StreamEngine/StreamAggregator.py:101-115) through a 4-field
+          MultiEncoder into a 4096-column SP (configs[4]).
+"""
+import numpy as np
+import pytest
+
+from test_gpu_parity import sp_equal, tm_equal
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+TRAIN = 300  # training records of the fleet's model (the oracle replays them too)
+
+
+@pytest.fixture(scope="module")
+def fleet_model(rt, oracle_mod, traces):
+    """Model 1 trained on the first TRAIN records, on the GPU and in the oracle
+    (bit-exact to each other: test_gpu_parity), then TM learning off as in
+    ModelTesting (NetworkModel.py:40-44)."""
+    tr = np.asarray(traces["train"][:TRAIN], np.float64)
+    eng = rt.HTMEngine(1, seg_capacity=1 << 14)
+    eng.run(torch.tensor(tr, device="cuda").reshape(-1, 1))
+    eng.status()
+    orc = oracle_mod.OracleModel()
+    for x in tr:
+        orc.step([x], True, True)
+    return eng, orc
+
+
+def fleet_inputs(traces, n, T, seed=29):
+    rng = np.random.default_rng(seed)
+    test = np.asarray(traces["test"], np.float64)
+    t = np.arange(T)[:, None]
+    s = np.arange(n)[None, :]
+    v = np.clip(test[(t + 37 * s) % len(test)] + rng.integers(-2, 3, size=(T, n)), 0, 100)
+    v[rng.random(v.shape) < 0.01] = np.nan
+    return v
+
+
+def test_config4_fleet_131072_streams_vs_oracle(rt, fleet_model, traces):
+    """131,072 streams share the frozen model (SP and TM learning off); 8
+    sampled streams replayed by independent oracle clones of the trained
+    model over 64 lockstep steps; streams 2^16.. repeat the inputs of streams
+    0.. and must repeat their scores; a one-stream fleet on one stream's
+    inputs gives that stream's scores (no cross-stream interference)."""
+    model, orc = fleet_model
+    n, T = 131072, 64
+    vals = fleet_inputs(traces, n // 2, T)
+    vals = np.concatenate([vals, vals], axis=1)  # identical-input pairs s, s + 65536
+    fl = rt.HTMEngine.fleet(model, n, q_capacity=4096)
+    v = torch.tensor(vals, device="cuda")
+    got = np.stack([fl.step(v[k]).cpu().numpy() for k in range(T)])
+    fl.status()
+    assert np.array_equal(got[:, : n // 2], got[:, n // 2:])
+    sample = [0, 1, 4097, 20011, 33333, 65535, 65536 + 777, n - 1]
+    for s in sample:
+        o = orc.clone()
+        want = np.array([o.step([vals[k, s]], False, False) for k in range(T)], np.float32)
+        assert np.array_equal(got[:, s], want), f"stream {s}"
+    solo = rt.HTMEngine.fleet(model, 1, q_capacity=4096)
+    s = 20011
+    one = np.array([solo.step(torch.tensor(vals[k, s:s + 1], device="cuda")).cpu().numpy()[0] for k in range(T)])
+    assert np.array_equal(one, got[:, s])
+    # the score distribution is not degenerate (the model predicts something)
+    assert 0 < np.count_nonzero(got == 0) < got.size
+
+
+def test_config3_many_fresh_streams_learning(rt, oracle_mod):
+    """512 fresh streams (seed per stream) with SP+TM learning on: 8 sampled
+    streams match independent oracle models at every step; two of them match
+    in their whole SP/TM state at the end."""
+    n, T = 512, 120
+    eng = rt.HTMEngine(n, seed_stride=1, seg_capacity=1 << 13)
+    rng = np.random.default_rng(41)
+    base = rng.integers(0, 101, size=(40, 1)).astype(np.float64)
+    vals = np.clip(np.tile(base, (3, n)) + rng.integers(-4, 5, size=(T, n)), 0, 100)
+    vals[rng.random(vals.shape) < 0.02] = np.nan
+    v = torch.tensor(vals, device="cuda")
+    eng.set_learning(True, True)
+    got = np.stack([eng.step(v[k]).cpu().numpy() for k in range(T)])
+    eng.status()
+    sample = [0, 3, 64, 127, 200, 311, 448, n - 1]
+    orcs = {s: oracle_mod.OracleModel(sp_seed=2045 + s, tm_seed=2045 + s) for s in sample}
+    for s, o in orcs.items():
+        want = np.array([o.step([vals[k, s]], True, True) for k in range(T)], np.float32)
+        assert np.array_equal(got[:, s], want), f"stream {s}"
+    for s in (sample[2], sample[-1]):
+        sp_equal(eng, s, orcs[s])
+        tm_equal(eng, s, orcs[s])
+
+
+# response times in ms next to cpu/mem percent: per-field encoder ranges
+FIELDS = [("cpu", 0.0, 100.0), ("max", 0.0, 5000.0), ("mean", 0.0, 2000.0), ("mem", 0.0, 100.0)]
+
+
+def aggregate_records(traces, T, seed=13):
+    """cpu/mem from the reference's traces; mean/max response time (ms) a noisy
+    function of load, the shape StreamAggregator emits."""
+    rng = np.random.default_rng(seed)
+    cpu = np.asarray(traces["train"][:T], np.float64)
+    mem = np.clip(0.6 * cpu + 20 + rng.normal(0, 3, T), 0, 100)
+    mean = np.clip(150 + 12 * cpu + rng.normal(0, 40, T), 0, None)
+    mx = np.clip(mean * rng.uniform(1.5, 3.0, T), 0, None)
+    return np.stack([cpu, mx, mean, mem], axis=1)
+
+
+def test_config5_four_field_aggregate_4096_columns(rt, oracle_mod, traces):
+    """cpu / max / mean / mem (sorted field order, per-field ranges) through
+    the 4-field encoder into the 4096-column SP, learning on, then TM learning
+    off; bit-exact against the oracle every step and in the final state."""
+    rec = aggregate_records(traces, 200)
+    rec[7, 1] = np.nan  # a missing aggregate field
+    mins = tuple(f[1] for f in FIELDS)
+    maxs = tuple(f[2] for f in FIELDS)
+    eng = rt.HTMEngine(1, n_fields=4, sp_columns=4096, seg_capacity=1 << 13,
+                       field_minval=mins, field_maxval=maxs)
+    orc = oracle_mod.OracleModel(n_fields=4, sp_columns=4096)
+    for f in range(4):
+        orc.params.field_minval[f], orc.params.field_maxval[f] = mins[f], maxs[f]
+    orc = oracle_mod.OracleModel(orc.params)
+    # the per-field ranges reach the encoder: field 1 = max response time
+    x = [50.0, 2500.0, 1000.0, 50.0]
+    sdr = orc.encode(x)
+    for f in range(4):
+        res = (maxs[f] - mins[f]) / (500 - 21)  # ScalarEncoder resolution (Appendix A.1)
+        assert np.nonzero(sdr[500 * f:500 * (f + 1)])[0][0] == int(((x[f] - mins[f]) + res / 2.0) / res)
+    for part, (sp_l, tm_l) in ((rec[:150], (True, True)), (rec[150:], (True, False))):
+        eng.set_learning(sp_l, tm_l)
+        for k in range(part.shape[0]):
+            g = eng.step(torch.tensor(part[k], device="cuda")).cpu().numpy()[0]
+            o = orc.step(part[k], sp_l, tm_l)
+            assert g == o, f"record {k}: gpu {g} oracle {o}"
+    sp_equal(eng, 0, orc)
+    tm_equal(eng, 0, orc)

@@ -233,3 +233,23 @@ def test_multilevel_facade_matches_engine_pair_and_reloads(rt, traces, tmp_path,
         assert a == net2.regions[ref.L2_TMR].getOutputData("anomalyScore")[0], f"step {k}"
         assert np.array_equal(net.regions[ref.L2_CLS].getOutputData("probabilities"),
                               net2.regions[ref.L2_CLS].getOutputData("probabilities"))
+
+
+def test_four_field_aggregate_encoder_with_per_field_ranges(rt):
+    """north_star's cpu %, mem %, mean and max response time (StreamAggregator.py:101-115):
+    fields share n/w/clipInput, each keeps its own [minval, maxval]."""
+    enc = rt.MultiEncoder()
+    spec = {k: {"fieldname": k, "type": "ScalarEncoder", "name": k, "minval": 0.0, "maxval": hi,
+                "clipInput": True, "w": 21, "n": 500}
+            for k, hi in (("cpu", 100.0), ("mem", 100.0), ("mean", 2000.0), ("max", 5000.0))}
+    enc.addMultipleEncoders(spec)
+    cfg = rt.network.engine_config(enc, dict(ref.SP_PARAMS, inputWidth=2000, columnCount=4096),
+                                   dict(ref.TM_PARAMS, columnCount=4096, inputWidth=4096)).as_dict()
+    names = [f.name for f in enc.fields()]
+    assert cfg["n_fields"] == 4 and cfg["sp_columns"] == 4096
+    assert cfg["field_maxval"] == [dict(cpu=100.0, mem=100.0, mean=2000.0, max=5000.0)[k] for k in names]
+    spec["mem"]["w"] = 11
+    bad = rt.MultiEncoder()
+    bad.addMultipleEncoders(spec)
+    with pytest.raises(ValueError):
+        rt.network.engine_config(bad, dict(ref.SP_PARAMS, inputWidth=1990), ref.TM_PARAMS)

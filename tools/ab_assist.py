@@ -1,8 +1,9 @@
 """A/B of engine variants on the config-2 lockstep workload: one engine per
 setting fed the same inputs, timed in interleaved rounds in one process
 (cdna_hip_programming.md §5.4 rule 24).  A setting "a:t:f:g" = HTM_OPT_BT_ASSIST
-a, HTM_OPT_BT_TAIL t, HTM_FX_MODE f, HTM_FX_GRAN g (the last two are read
-when the engine is created; g = 0 keeps the default)."""
+a, HTM_OPT_BT_TAIL t, HTM_FX_MODE f, HTM_FX_GRAN g, HTM_FX_PID p (the last
+three are read when the engine is created; g = 0 keeps the default, p = 0
+drops the pid lists)."""
 import json
 import os
 import sys
@@ -26,7 +27,8 @@ trace = d["test_cpu"].astype(np.float64)
 base, _, _, _ = bench.trained_engine(rt, 1, 72 * 1024, 0, train)
 engs = {}
 for m in modes:
-    a_, t_, f_, g_ = (int(x) for x in (m + ":0:0:0").split(":")[:4])
+    a_, t_, f_, g_, p_ = (int(x) for x in (m + ":0:0:0:1").split(":")[:5])
+    os.environ["HTM_FX_PID"] = str(p_)
     os.environ["HTM_FX_MODE"] = str(f_)
     if g_:
         os.environ["HTM_FX_GRAN"] = str(g_)
