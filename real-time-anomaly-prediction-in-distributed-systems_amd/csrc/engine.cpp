@@ -240,8 +240,6 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
     // bitonic key sort at Model-1 sizes
     d.fin_mode = 2;
-    d.fx_mode = 0;
-    if (const char* env = std::getenv("HTM_FX_MODE")) d.fx_mode = std::atoi(env) & 7;  // A/B knob
     if (const char* env = std::getenv("HTM_TM_FIN"))
         d.fin_mode = std::strcmp(env, "sorted") == 0 ? 1 : std::strcmp(env, "buckets") == 0 ? 0 : 2;
     // frozen-inference counter window: the union region holds the u8
@@ -537,6 +535,8 @@ static int alloc_fx(htm_engine* e) {
     ALLOC(e->tm.scr_cur, uint32_t, M * (size_t)d.fx_noff);
     ALLOC(e->tm.fx_off, uint32_t, M * (size_t)d.fx_noff);
     ALLOC(e->tm.fx_rec, uint2, M * (size_t)d.seg_cap);
+    ALLOC(e->tm.fx_rslot, uint32_t, M * (size_t)d.seg_cap);
+    ALLOC(e->tm.fx_nr, uint32_t, M);
     ALLOC(e->tm.fx_pcell, uint16_t, M * (size_t)d.fx_pcap);
     ALLOC(e->tm.fx_np, uint32_t, M);
     return HTM_OK;
@@ -546,6 +546,7 @@ static int build_fx(htm_engine* e, hipStream_t st) {
     const DevCfg& d = e->dc;
     int ra = alloc_fx(e);
     if (ra) return ra;
+    if (launch_tm_fx_rank(d, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "fx rank launch");
     if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return htm_fail(HTM_E_HIP, "fx count launch");
     std::vector<uint64_t> counts((size_t)e->nm);
     HIP_TRY(hipMemcpyAsync(counts.data(), e->d_counts, counts.size() * 8, hipMemcpyDeviceToHost, st));

@@ -28,10 +28,6 @@
 #endif
 #define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
 #define FX_MAXPER ((HTM_MAXACT * HTM_MAXK + TM_NT - 1) / TM_NT)  // active cells per thread
-#ifndef HTM_FX_PUSH
-#define HTM_FX_PUSH 1              // 1: qualify segments as their counters reach the threshold (returning
-                                   //    LDS atomics); 0: count with plain atomics, then sweep the counters
-#endif
 
 // Derived, immutable engine constants (kernel argument).
 struct DevCfg {
@@ -66,9 +62,6 @@ struct DevCfg {
     int32_t n_streams;
     int32_t shared_model;                 // fleet: every stream reads model instance 0 (SP + TM frozen)
     int32_t q_cap;                        // per-stream capacity of the qualifying-segment scratch lists
-    int32_t fx_mode;                      // frozen counting: bit 0 masked padding, bit 1 wave-aggregated
-                                          // qualification (fx_count_block_push); bit 2 rewrite the
-                                          // dutyCycle record on every frozen step (no FX_FRESH)
     int32_t sdr_in;                       // the SP reads an external input SDR of nin bits (no encoder)
 };
 
@@ -108,11 +101,14 @@ struct TmBufs {
     uint32_t* scr_q2;       // [S][q_cap] (>= seg_cap entries): bucket-sorted keys / index-build pid map
     uint8_t* prev_pred;     // [S][ncol] nonzero(colConf(t-1)) captured before compute
     uint32_t* scr_cur;      // [S][ncells*fx_nwin] frozen-index fill cursors
-    // frozen forward index (valid while TM learning is off): for stream s,
-    // cell x and counter window w, the window-relative slots (u16) of the
-    // segments with a synapse from x fill the 16-byte blocks
-    // fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1]), padded
-    // with 0xFFFF, so one uint4 load delivers 8 entries of one list
+    // frozen forward index (valid while TM learning is off).  Live segments
+    // are numbered by RANK in NuPIC's (cell, creation) order -- the order
+    // _inferPhase2 sums confidences in -- so segments that qualify, found by a
+    // sweep over rank-ordered counters, come out already in summation order.
+    // For stream s, cell x and counter window w (a range of fx_win ranks), the
+    // window-relative ranks (u16) of the segments with a synapse from x fill
+    // the 16-byte blocks fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1]),
+    // padded with 0xFFFF, so one uint4 load delivers 8 entries of one list
     // The same block pool also holds, per cell, the list of predictive-
     // capable segment ids (pid: live segments with >= activationThreshold
     // connected synapses, numbered densely in slot order) that the cell
@@ -123,7 +119,9 @@ struct TmBufs {
     uint64_t* fx_base;      // [S] first block of the stream
     uint32_t* fx_off;       // [S][fx_noff]: [cell][window] lists, then [cell] pid lists, then the end
     uint4* fx_ent;          // [total blocks] 8 x u16 entries each
-    uint2* fx_rec;          // [S][seg_cap] {cell | FX_FRESH, dutyCycle bits}
+    uint2* fx_rec;          // [S][seg_cap] by rank: {cell | FX_FRESH, dutyCycle bits}
+    uint32_t* fx_rslot;     // [S][seg_cap] pool slot of each rank
+    uint32_t* fx_nr;        // [S] ranks (live segments)
     uint16_t* fx_pcell;     // [S][fx_pcap] cell of each pid
     uint32_t* fx_np;        // [S] number of pids (> fx_pcap: pid lists not built, rows are read)
     uint64_t* dbg;          // [S][32] phase stamps + event counts (HTM_STAMPS builds only, else null)
@@ -335,6 +333,7 @@ int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int l
                    hipStream_t st);
 int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,
                        hipStream_t st);
+int launch_tm_fx_rank(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_init(const DevCfg& c, const TmBufs& b, const uint64_t* seeds, int n, hipStream_t st);
 int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen,
                    int n, hipStream_t st);

@@ -87,8 +87,10 @@ struct Tm {
     const uint32_t* fxoff;
     const uint4* fxent;
     const uint2* fxrec;
+    const uint32_t* fxrslot;
     const uint16_t* fxpcell;
     uint32_t np;       // predictive-capable segments (pids) of this stream
+    uint32_t nr;       // ranks (live segments) of the frozen index
     const TmBufs* tb;  // the engine's buffers (backtrack assist)
     uint32_t bt_epoch; // > 0: this launch's backtracks are assisted (frozen lockstep)
 };
@@ -349,10 +351,10 @@ __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int t
     STAMP(t, SB_SCAN);
 }
 
-// one 16-byte block of a frozen out-list: 8 window-relative u16 slots,
-// 0xFFFF = padding; bump the slot's u8 counter
-// (padding is counted branch-free into a per-lane spare word past the
-// counters, cnt[dummy + lane], so sink updates never collide)
+// one 16-byte block of a frozen out-list: 8 window-relative u16 ranks,
+// 0xFFFF = padding; bump the rank's u8 counter with non-returning LDS
+// atomics (padding is counted branch-free into a per-lane spare word past
+// the counters, cnt[dummy + lane], so sink updates never collide)
 __device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v, uint32_t dummy) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -362,109 +364,15 @@ __device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v, uint32_t 
     }
 }
 
-// Every counter byte >= thr of cnt[0 .. nbytes) (nbytes a multiple of 16) as
-// slot base + index appended to dst at *qn (dense sweep after counting with
-// non-returning atomics; HTM_FX_PUSH=0 builds).
-__device__ __forceinline__ void fx_collect_dense(const uint32_t* cnt, uint32_t nbytes, uint32_t thr, uint32_t base,
-                                                 int32_t* qn, uint32_t* dst, uint32_t qcap) {
-    const uint32_t add = 0x01010101u * (128u - thr);
-    const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
-    const uint32_t n16 = nbytes / 16;
-    constexpr int U = 4;  // quads in flight per thread
-    for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += U * TM_NT) {
-        uint4 x[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t i = i0 + u * TM_NT;
-            x[u] = i < n16 ? c4[i] : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t i = i0 + u * TM_NT;
-            uint32_t m[4] = {(x[u].x + add) & 0x80808080u, (x[u].y + add) & 0x80808080u,
-                             (x[u].z + add) & 0x80808080u, (x[u].w + add) & 0x80808080u};
-            if (i >= n16) m[0] = m[1] = m[2] = m[3] = 0u;
-            if ((m[0] | m[1] | m[2] | m[3]) == 0u) continue;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                for (uint32_t y = m[q]; y; y &= y - 1) {
-                    const uint32_t k = (uint32_t)atomicAdd(qn, 1);
-                    if (k < qcap) dst[k] = base + 16 * i + 4 * q + ((__ffs(y) - 1) >> 3);
-                }
-            }
-        }
-    }
-}
-
-// the same, and every counter that reaches thr (it happens once: counters
-// only grow) appends base + slot to dst at *qn -- qualification without a
-// sweep over the counters
-// fx_mode bit 0: padding entries skip the atomic (exec-masked) instead of
-// adding into the lane's sink word; bit 1: qualifying segments reserve their
-// list positions with one LDS atomic per wave (ballot ranks) instead of one
-// same-address atomic per lane
-__device__ __forceinline__ void fx_count_block_push(uint32_t* cnt, uint4 v, uint32_t thr, uint32_t base, int32_t* qn,
-                                                    uint32_t* dst, uint32_t qcap, uint32_t dummy, int fx_mode) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t old[8];
-    if (fx_mode & 1) {
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-            old[h] = 0u;
-            if (rel != 0xFFFFu) old[h] = atomicAdd(&cnt[rel >> 2], 1u << ((rel & 3) * 8));
-        }
-    } else {
-#pragma unroll
-        for (int h = 0; h < 8; h++) {  // branch-free: padding goes to the lane's sink word
-            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-            old[h] = atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy + (threadIdx.x & 63)], 1u << ((rel & 3) * 8));
-        }
-    }
-    if (fx_mode & 2) {
-        uint32_t qmask = 0;
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-            if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) qmask |= 1u << h;
-        }
-        const uint32_t nq = __popc(qmask);
-        const uint32_t tot = wave_sum_u32(nq);
-        if (tot) {  // wave-uniform
-            const uint32_t pre = wave_incl_scan(nq) - nq;
-            uint32_t b0 = 0;
-            if (lane_id() == 0) b0 = (uint32_t)atomicAdd(qn, (int32_t)tot);
-            b0 = __shfl(b0, 0, 64) + pre;
-            for (uint32_t x = qmask; x; x &= x - 1) {
-                const int h = __ffs(x) - 1;
-                const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-                if (b0 < qcap) dst[b0] = base + rel;
-                b0++;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-            const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-            if (rel != 0xFFFFu && ((old[h] >> ((rel & 3) * 8)) & 0xFFu) == thr - 1u) {
-                const uint32_t i = (uint32_t)atomicAdd(qn, 1);
-                if (i < qcap) dst[i] = base + rel;
-            }
-        }
-    }
-}
-
 // Stream the 16-byte blocks of lists k < na -- list k is the block range
 // [plo[k], plo[k] + n_k) of ent, pstart the exclusive prefix of n_k with
 // pstart[na] = B -- and count every u16 entry into the u8 counters.  Per
 // pass a block -> list map is built in LDS, then every thread issues its
 // FX_DEPTH block loads before counting any, so one HBM round trip covers
 // FX_OWN blocks whatever the list lengths.
-template <bool PUSH>
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
-                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy, uint32_t thr = 0,
-                                          uint32_t base = 0, int32_t* qn = nullptr, uint32_t* dst = nullptr,
-                                          uint32_t qcap = 0, TmSh* shp = nullptr, int fx_mode = 0) {
+                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy,
+                                          TmSh* shp = nullptr) {
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
         for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
@@ -492,8 +400,7 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
                 STAMP_SH(shp, SB_SLOAD);
             }
 #endif
-            if (PUSH) fx_count_block_push(cnt, v[j], thr, base, qn, dst, qcap, dummy, fx_mode);
-            else fx_count_block(cnt, v[j], dummy);
+            fx_count_block(cnt, v[j], dummy);
         }
         STAMP_SH(shp, SB_COUNT);
         __syncthreads();
@@ -517,49 +424,40 @@ __device__ __forceinline__ void fx_qualify(const uint32_t* cnt, uint32_t nbytes,
     }
 }
 
-// The counter bytes >= thr of cnt[0 .. nbytes) as slots base + index,
-// appended to dst at *qn.  A first sweep counts each wave's hits (one LDS
-// atomic per wave reserves its range), a second writes them, ranked within
-// the wave by ballot bit counts -- no per-iteration scans or atomics.
-__device__ __forceinline__ void fx_collect(const uint32_t* cnt, uint32_t nbytes, uint32_t thr, uint32_t base,
-                                           int32_t* qn, uint32_t* dst) {
+// The counter bytes >= thr of the nquads 16-byte quads at cnt, as ranks
+// base + index, appended to dst at sh->qn in ASCENDING order (each thread
+// sweeps a contiguous run of quads; one workgroup scan places the runs), so
+// the qualifying list comes out in rank = (cell, creation) order.  Counters
+// never exceed 32 (see fx_qualify).  Contains barriers: call uniformly.
+__device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t nquads, uint32_t thr, uint32_t base,
+                                                   TmSh* sh, uint32_t* dst, uint32_t qcap) {
     const uint32_t add = 0x01010101u * (128u - thr);
     const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
-    const uint32_t n16 = nbytes / 16;
+    const uint32_t per = (nquads + TM_NT - 1) / TM_NT;
+    const uint32_t q0 = threadIdx.x * per;
+    const uint32_t q1 = q0 + per < nquads ? q0 + per : nquads;
     uint32_t mine = 0;
-    for (uint32_t i = threadIdx.x; i < n16; i += TM_NT) {
-        const uint4 x = c4[i];
+    for (uint32_t q = q0; q < q1; q++) {
+        const uint4 x = c4[q];
         mine += __popc((x.x + add) & 0x80808080u) + __popc((x.y + add) & 0x80808080u) +
                 __popc((x.z + add) & 0x80808080u) + __popc((x.w + add) & 0x80808080u);
     }
-    const uint32_t wtot = wave_sum_u32(mine);
-    if (wtot == 0) return;  // wave-uniform
-    uint32_t pos = 0;
-    if (lane_id() == 0) pos = (uint32_t)atomicAdd(qn, (int32_t)wtot);
-    pos = __shfl(pos, 0, 64);
-    for (uint32_t i0 = 0; i0 < n16; i0 += TM_NT) {
-        const uint32_t i = i0 + threadIdx.x;
-        uint32_t m[4] = {0u, 0u, 0u, 0u};
-        if (i < n16) {
-            const uint4 x = c4[i];
-            m[0] = (x.x + add) & 0x80808080u;
-            m[1] = (x.y + add) & 0x80808080u;
-            m[2] = (x.z + add) & 0x80808080u;
-            m[3] = (x.w + add) & 0x80808080u;
-        }
-        for (;;) {
-            const int q = m[0] ? 0 : m[1] ? 1 : m[2] ? 2 : m[3] ? 3 : -1;
-            const uint64_t bal = __ballot(q >= 0);
-            if (!bal) break;
-            if (q >= 0) {
-                const uint32_t x = q == 0 ? m[0] : q == 1 ? m[1] : q == 2 ? m[2] : m[3];
-                dst[pos + ballot_rank(bal)] = base + 16 * i + 4 * q + ((__ffs(x) - 1) >> 3);
-                const uint32_t y = x & (x - 1);
-                if (q == 0) m[0] = y; else if (q == 1) m[1] = y; else if (q == 2) m[2] = y; else m[3] = y;
+    const uint32_t qn0 = (uint32_t)sh->qn;  // thread 0 updates it only after the barrier below
+    uint32_t tot;
+    uint32_t pos = qn0 + wg_excl_scan(sh, mine, &tot);
+    for (uint32_t q = q0; q < q1 && mine; q++) {
+        const uint4 x = c4[q];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            for (uint32_t m = (w[j] + add) & 0x80808080u; m; m &= m - 1) {
+                if (pos < qcap) dst[pos] = base + 16 * q + 4 * j + ((__ffs(m) - 1) >> 3);
+                pos++;
             }
-            pos += (uint32_t)__popcll(bal);
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) sh->qn = (int32_t)(qn0 + tot);
 }
 
 // zero n 16-byte quads of LDS
@@ -587,11 +485,11 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
     const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
     const uint32_t na = nact < mac ? nact : mac;
-    const uint32_t hwm = sh->hwm;
+    const uint32_t nr = t.nr;
     STAMP(t, SB_LIST);
     COUNT(t, SC_NACT, na);
     const uint32_t nwin = (uint32_t)c.fx_nwin;
-    const uint32_t nw = (hwm + W - 1) / W;
+    const uint32_t nw = (nr + W - 1) / W;
     const bool pid_ok = t.np <= (uint32_t)c.fx_pcap;
     const uint32_t per = (na + TM_NT - 1) / TM_NT;  // <= FX_MAXPER (na <= 64 x 32)
     const uint32_t k0 = threadIdx.x * per;
@@ -650,26 +548,17 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         }
         if (threadIdx.x == 0) pstart[na] = B;
         nblk += B;
-        const uint32_t nbytes = w < 0 ? (t.np + 15u) & ~15u : W;
+        // counters cover the pids (pass -1) or this window's ranks
+        const uint32_t span = w < 0 ? t.np : (nr - (uint32_t)w * W < W ? nr - (uint32_t)w * W : W);
+        const uint32_t nbytes = (span + 15u) & ~15u;
         wg_clear4(cnt, nbytes / 16);
         __syncthreads();
         STAMP(t, SB_WINPRE);
         COUNT(t, SC_WIN, 1);
         COUNT(t, SC_BLK, B);
-#if HTM_FX_PUSH
-        if (w < 0) fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, 0, 0, nullptr, nullptr, 0, sh);
-        else
-            fx_stream<true>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, (uint32_t)thr, (uint32_t)w * W, &sh->qn,
-                            t.q1, (uint32_t)c.q_cap, sh, c.fx_mode);
+        fx_stream(t.fxent, plo, pstart, na, B, cnt, owner, dummy, sh);
         STAMP(t, SB_STREAM);
-#else
-        fx_stream<false>(t.fxent, plo, pstart, na, B, cnt, owner, dummy, 0, 0, nullptr, nullptr, 0, sh);
-        STAMP(t, SB_STREAM);
-        if (w >= 0) {
-            fx_collect_dense(cnt, nbytes, (uint32_t)thr, (uint32_t)w * W, &sh->qn, t.q1, (uint32_t)c.q_cap);
-            __syncthreads();
-        }
-#endif
+        if (w >= 0) fx_collect_ordered(cnt, nbytes / 16, (uint32_t)thr, (uint32_t)w * W, sh, t.q1, (uint32_t)c.q_cap);
         if (w < 0) {
             // pid counter >= activationThreshold: the segment's cell is predicted
             const uint32_t np = t.np;
@@ -701,24 +590,27 @@ __device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
     const bool fx_pid = FROZEN && t.np <= (uint32_t)c.fx_pcap;
     for (uint32_t k = threadIdx.x; k < qn && fx_pid; k += TM_NT) {
         // frozen index: cell and the (frozen-iteration) dutyCycle of the
-        // segment.  The dutyCycle() state update is a store of the value it
-        // returns.
-        const uint32_t slot = t.q1[k];
-        const uint2 rec = t.fxrec[slot];
+        // segment of rank q1[k].  The dutyCycle() state update is a store of
+        // the value it returns.
+        const uint32_t rank = t.q1[k];
+        const uint2 rec = t.fxrec[rank];
         // the dutyCycle() state write stores the same value every time while
         // the iteration counter is frozen: only the first one after the index
         // build changes the record (FX_FRESH marks it done, or never needed)
-        if (!(rec.x & FX_FRESH) || (c.fx_mode & 4)) {  // (fx_mode bit 2: write every time, A/B)
+        if (!(rec.x & FX_FRESH)) {
+            const uint32_t slot = t.fxrslot[rank];
             t.duty[(size_t)slot * 3 + 1] = rec.y;
             t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
-            if (!(c.fx_mode & 4)) atomicOr(const_cast<uint32_t*>(&t.fxrec[slot].x), FX_FRESH);
-            nb += 8u;
+            atomicOr(const_cast<uint32_t*>(&t.fxrec[rank].x), FX_FRESH);
+            nb += 12u;
         }
         nb += 8u;
-        emit(k, slot, rec.x & 0xFFFFu, __uint_as_float(rec.y));
+        emit(k, rank, rec.x & 0xFFFFu, __uint_as_float(rec.y));
     }
     for (uint32_t k = threadIdx.x; k < qn && !fx_pid; k += TM_NT) {
-        uint32_t slot = t.q1[k];
+        // q1 holds ranks (frozen) or pool slots (learning scan)
+        uint32_t slot = FROZEN ? t.fxrslot[t.q1[k]] : t.q1[k];
+        if (FROZEN) nb += 4u;
         uint32_t m = t.meta[slot];
         uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
         // meta + conn + used source rows + duty-cycle record read and written
@@ -827,10 +719,85 @@ __device__ __forceinline__ uint32_t phase2_finish_sorted(Tm& t, uint32_t qn) {
     return npcol;
 }
 
+// Tail of the frozen _inferPhase2: the qualifying segments arrive in rank =
+// (column, cell, creation) order -- NuPIC's summation order -- so each
+// column's confidence is the in-order float sum over its run of the list and
+// the normaliser folds the run sums in ascending column order: bit-identical
+// to the oracle without sorting.  Column and dutyCycle of entry k live in
+// LDS (qn <= q_lds) or, past that, in the HBM scratch (q1 / q2).  Returns
+// numPredictedCols.
+__device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const uint32_t qn = (uint32_t)sh->qn;
+    const uint32_t ql = (uint32_t)c.q_lds;
+    const bool in_lds = qn <= ql;
+    uint16_t* lcol = reinterpret_cast<uint16_t*>(t.U);  // [ql]
+    float* ldc = reinterpret_cast<float*>(t.U + (ql + 1) / 2);  // [ql]
+    uint32_t* gcol = t.q1;
+    float* gdc = reinterpret_cast<float*>(t.q2);
+    uint32_t nb = phase2_pass1<true>(t, qn, [&](uint32_t k, uint32_t, uint32_t cell, float dc) {
+        const uint32_t col = col_of(c, cell);
+        if (in_lds) {
+            lcol[k] = (uint16_t)col;
+            ldc[k] = dc;
+        } else {  // q1[k] (the rank) has been read: reuse the entry
+            gcol[k] = col;
+            gdc[k] = dc;
+        }
+    });
+    nb = wg_sum(sh, nb);  // (barriers)
+    if (threadIdx.x == 0) sh->bytes += nb;
+    STAMP(t, SB_FIN1);
+    COUNT(t, SC_QN, qn);
+    COUNT(t, SC_P2, 1);
+    auto col_at = [&](uint32_t k) -> uint32_t { return in_lds ? (uint32_t)lcol[k] : gcol[k]; };
+    auto dc_at = [&](uint32_t k) -> float { return in_lds ? ldc[k] : gdc[k]; };
+    // run heads sum their column in list order
+    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+        const uint32_t col = col_at(k);
+        if (k > 0 && col_at(k - 1) == col) continue;
+        float sum = 0.0f;
+        for (uint32_t j = k; j < qn && col_at(j) == col; j++) sum += dc_at(j);
+        t.colconf[col] = sum;
+    }
+    __syncthreads();
+    STAMP(t, SB_SUMS);
+    // normaliser: sequential over the columns with a qualifying segment,
+    // ascending (= run-head order); wave 0 loads 64 entries at a time and
+    // folds them lane by lane, non-heads adding +0.0f (the sum is unchanged)
+    if (wave_id() == 0) {
+        float tot = 0.0f;
+        for (uint32_t base = 0; base < qn; base += 64) {
+            const uint32_t i = base + lane_id();
+            float v = 0.0f;
+            if (i < qn) {
+                const uint32_t col = col_at(i);
+                if (i == 0 || col_at(i - 1) != col) v = t.colconf[col];
+            }
+            const int vi = __float_as_int(v);
+#pragma unroll
+            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
+        }
+        if (lane_id() == 0) sh->tf[0] = tot;
+    }
+    __syncthreads();
+    const float tot = sh->tf[0];
+    if (tot > 0.0f)
+        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+            const uint32_t col = col_at(k);
+            if (k == 0 || col_at(k - 1) != col) t.colconf[col] /= tot;
+        }
+    const uint32_t npcol = count_predicted_cols(t);  // (barriers)
+    STAMP(t, SB_FIN2);
+    return npcol;
+}
+
 // Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
 // NuPIC order, normalisation.  Returns numPredictedCols (uniform).
 template <bool FROZEN>
 __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
+    if (FROZEN) return phase2_finish_ranked(t);
     if (t.c.fin_mode == 1 && (uint32_t)t.sh->qn <= (uint32_t)t.c.q_lds)
         return phase2_finish_sorted<FROZEN>(t, (uint32_t)t.sh->qn);
     const DevCfg& c = t.c;
@@ -2019,14 +1986,18 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
         t.fxoff = b.fx_off + ms * (size_t)c.fx_noff;
         t.fxent = b.fx_ent + b.fx_base[ms];
         t.fxrec = b.fx_rec + ms * sc;
+        t.fxrslot = b.fx_rslot + ms * sc;
         t.fxpcell = b.fx_pcell + ms * c.fx_pcap;
         t.np = b.fx_np[ms];
+        t.nr = b.fx_nr[ms];
     } else {
         t.fxoff = nullptr;
         t.fxent = nullptr;
         t.fxrec = nullptr;
+        t.fxrslot = nullptr;
         t.fxpcell = nullptr;
         t.np = 0;
+        t.nr = 0;
     }
     t.tb = &b;
     t.bt_epoch = 0;
@@ -2636,41 +2607,104 @@ __device__ __forceinline__ float seg_dc_peek(const uint32_t* duty, uint32_t slot
     return pow_det((float)(1.0 - (double)alpha), age) * last;
 }
 
+// Ranks: live segments in (cell, slot) order -- slot order within a cell is
+// creation order, NuPIC's segment list order.  Counting sort by cell (counts
+// and cursors in scr_cur), then each cell's few slots sorted in place.
+__global__ void tm_fx_rank_kernel(DevCfg c, TmBufs b) {
+    const int s = blockIdx.x;
+    const size_t sc = (size_t)c.seg_cap;
+    const uint32_t* meta = b.seg_meta + (size_t)s * sc;
+    uint32_t* cnt = b.scr_cur + (size_t)s * c.fx_noff;  // ncells + 1 <= fx_noff
+    uint32_t* rslot = b.fx_rslot + (size_t)s * sc;
+    const uint32_t hwm = b.hdr[s].seg_hwm;
+    const uint32_t nc = (uint32_t)c.ncells;
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t tot;
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) cnt[i] = 0u;
+    __syncthreads();
+    for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
+        const uint32_t m = meta[slot];
+        if (meta_live(m)) atomicAdd(&cnt[meta_cell(m)], 1u);
+    }
+    __syncthreads();
+    const uint32_t per = (nc + blockDim.x - 1) / blockDim.x;
+    const uint32_t i0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per && i0 + k < nc; k++) sum += cnt[i0 + k];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < (int)blockDim.x; k++) { uint32_t v = part[k]; part[k] = run; run += v; }
+        tot = run;
+        b.fx_nr[s] = run;
+    }
+    __syncthreads();
+    uint32_t run = part[threadIdx.x];
+    for (uint32_t k = 0; k < per && i0 + k < nc; k++) {
+        const uint32_t v = cnt[i0 + k];
+        cnt[i0 + k] = run;
+        run += v;
+    }
+    __syncthreads();
+    for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
+        const uint32_t m = meta[slot];
+        if (meta_live(m)) rslot[atomicAdd(&cnt[meta_cell(m)], 1u)] = slot;
+    }
+    __syncthreads();
+    // cnt[x] is now the end of cell x's rank range
+    for (uint32_t x = threadIdx.x; x < nc; x += blockDim.x) {
+        const uint32_t lo = x ? cnt[x - 1] : 0u, hi = cnt[x];
+        for (uint32_t i = lo + 1; i < hi; i++) {
+            const uint32_t v = rslot[i];
+            uint32_t j = i;
+            while (j > lo && rslot[j - 1] > v) { rslot[j] = rslot[j - 1]; j--; }
+            rslot[j] = v;
+        }
+    }
+    (void)tot;
+}
+
+int launch_tm_fx_rank(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+    hipLaunchKernelGGL(tm_fx_rank_kernel, dim3(n), dim3(256), 0, st, c, b);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
     const int s = blockIdx.x;
     const size_t sc = (size_t)c.seg_cap;
     const uint32_t* meta = b.seg_meta + (size_t)s * sc;
     const uint16_t* src = b.seg_src + (size_t)s * sc * HTM_MAXSYN;
     const uint32_t* conn = b.seg_conn + (size_t)s * sc;
+    const uint32_t* rslot = b.fx_rslot + (size_t)s * sc;
     const size_t noff = (size_t)c.fx_noff;
     const size_t p0 = (size_t)c.ncells * c.fx_nwin;  // first pid-list counter
     uint32_t* off = b.fx_off + (size_t)s * noff;
-    uint32_t* pid = b.scr_q2 + (size_t)s * sc;
+    uint32_t* pid = b.scr_q2 + (size_t)s * sc;  // by rank
     uint16_t* pcell = b.fx_pcell + (size_t)s * c.fx_pcap;
-    const uint32_t hwm = b.hdr[s].seg_hwm;
+    const uint32_t nr = b.fx_nr[s];
     __shared__ uint32_t part[256];
     __shared__ uint32_t tot;
     for (size_t i = threadIdx.x; i < noff; i += blockDim.x) off[i] = 0u;
     __syncthreads();
     // window-list entry counts; predictive-capable flags over a contiguous
-    // chunk of slots per thread (pids are dense in slot order)
-    const uint32_t sper = (hwm + blockDim.x - 1) / blockDim.x;
-    const uint32_t s0 = threadIdx.x * sper, s1 = s0 + sper < hwm ? s0 + sper : hwm;
+    // chunk of ranks per thread (pids are dense in rank order)
+    const uint32_t rper = (nr + blockDim.x - 1) / blockDim.x;
+    const uint32_t r0 = threadIdx.x * rper, r1 = r0 + rper < nr ? r0 + rper : nr;
     uint32_t ncap = 0;
-    for (uint32_t slot = s0; slot < s1; slot++) {
+    for (uint32_t r = r0; r < r1; r++) {
+        const uint32_t slot = rslot[r];
         const uint32_t m = meta[slot];
+        const uint32_t nsyn = meta_nsyn(m), w = r / (uint32_t)c.fx_win;
+        for (uint32_t j = 0; j < nsyn; j++)
+            atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+        const uint32_t cm = conn[slot] & (nsyn >= 32 ? ~0u : ((1u << nsyn) - 1u));
         uint32_t p = ~0u;
-        if (meta_live(m)) {
-            const uint32_t nsyn = meta_nsyn(m), w = slot / (uint32_t)c.fx_win;
-            for (uint32_t j = 0; j < nsyn; j++)
-                atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
-            const uint32_t cm = conn[slot] & (nsyn >= 32 ? ~0u : ((1u << nsyn) - 1u));
-            if (__popc(cm) >= (uint32_t)c.act_thr) {
-                p = 0u;
-                ncap++;
-            }
+        if (__popc(cm) >= (uint32_t)c.act_thr) {
+            p = 0u;
+            ncap++;
         }
-        pid[slot] = p;
+        pid[r] = p;
     }
     part[threadIdx.x] = ncap;
     __syncthreads();
@@ -2684,10 +2718,11 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
     const uint32_t np = tot;
     if (np <= (uint32_t)c.fx_pcap) {
         uint32_t next = part[threadIdx.x];
-        for (uint32_t slot = s0; slot < s1; slot++) {
-            if (pid[slot] == ~0u) continue;
+        for (uint32_t r = r0; r < r1; r++) {
+            if (pid[r] == ~0u) continue;
+            const uint32_t slot = rslot[r];
             const uint32_t m = meta[slot], nsyn = meta_nsyn(m), cm = conn[slot];
-            pid[slot] = next;
+            pid[r] = next;
             pcell[next] = (uint16_t)meta_cell(m);
             next++;
             for (uint32_t j = 0; j < nsyn; j++)
@@ -2737,31 +2772,32 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
     const uint32_t* conn = b.seg_conn + (size_t)s * sc;
     const uint32_t* duty = b.seg_duty + (size_t)s * sc * 3;
     const uint32_t* pid = b.scr_q2 + (size_t)s * sc;
+    const uint32_t* rslot = b.fx_rslot + (size_t)s * sc;
     const size_t noff = (size_t)c.fx_noff;
     const size_t p0 = (size_t)c.ncells * c.fx_nwin;
     const uint32_t* off = b.fx_off + (size_t)s * noff;
     uint32_t* cur = b.scr_cur + (size_t)s * noff;
     uint16_t* ent = reinterpret_cast<uint16_t*>(b.fx_ent + b.fx_base[s]);
     uint2* rec = b.fx_rec + (size_t)s * sc;
-    const uint32_t hwm = b.hdr[s].seg_hwm;
+    const uint32_t nr = b.fx_nr[s];
     const uint32_t it = b.hdr[s].lrn_iter;
     const bool pid_ok = b.fx_np[s] <= (uint32_t)c.fx_pcap;
     const uint32_t W = (uint32_t)c.fx_win;
     for (size_t i = threadIdx.x; i + 1 < noff; i += blockDim.x) cur[i] = off[i] * 8u;
     __syncthreads();
-    for (uint32_t slot = threadIdx.x; slot < hwm; slot += blockDim.x) {
-        uint32_t m = meta[slot];
-        if (!meta_live(m)) continue;
-        uint32_t nsyn = meta_nsyn(m), w = slot / W;
+    for (uint32_t r = threadIdx.x; r < nr; r += blockDim.x) {
+        const uint32_t slot = rslot[r];
+        const uint32_t m = meta[slot];
+        const uint32_t nsyn = meta_nsyn(m), w = r / W;
         for (uint32_t j = 0; j < nsyn; j++) {
             uint32_t pos = atomicAdd(&cur[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
-            ent[pos] = (uint16_t)(slot - w * W);
+            ent[pos] = (uint16_t)(r - w * W);
         }
         // FX_FRESH: the record already holds what a frozen dutyCycle() stores
         // (lastDCIter == it past the first tier: age 0 returns without a write)
         const uint32_t fresh = (it > kDcTier[1] && duty[(size_t)slot * 3 + 2] == it) ? FX_FRESH : 0u;
-        rec[slot] = make_uint2(meta_cell(m) | fresh, __float_as_uint(seg_dc_peek(duty, slot, it)));
-        const uint32_t p = pid[slot];
+        rec[r] = make_uint2(meta_cell(m) | fresh, __float_as_uint(seg_dc_peek(duty, slot, it)));
+        const uint32_t p = pid[r];
         if (pid_ok && p != ~0u) {
             const uint32_t cm = conn[slot];
             for (uint32_t j = 0; j < nsyn; j++) {
