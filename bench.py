@@ -410,7 +410,10 @@ def main():
             # HBM bytes per launch measured by rocprofv3 --pmc passes of THIS command
             # (tools/pmc_summary.py, run in the same gpurun call; corrections there)
             pm = json.load(open(args.pmc_summary))
-            k = pm.get("kernels", {}).get(kernel_name(c3, c4, eng.fused))
+            base = kernel_name(c3, c4, eng.fused)
+            ks = [v for n, v in pm.get("kernels", {}).items()
+                  if n.split("(")[0].replace("void ", "").strip() == base and "hbm_bytes_per_dispatch" in v]
+            k = ks[0] if ks else None
             if k:
                 traffic = int(k["hbm_bytes_per_dispatch"])
                 tsrc = f"{args.pmc_summary}: {k.get('formula', '')}"
@@ -455,9 +458,11 @@ def main():
 
 
 def kernel_name(c3, c4, fused):
+    """The dominant kernel's name as rocprofv3 reports it (without the
+    argument list): the fused SP+TM kernel, frozen-TM or learning variant."""
     if not fused:
-        return "tm_step_kernel"
-    return ("htm_run_kernel<true> (fused SP+TM, learning)" if c3 else "htm_run_frozen_kernel (fused SP+TM, frozen TM)")
+        return "tm_step_kernel<false, true>" if not c3 else "tm_step_kernel<true, false>"
+    return "htm_run_kernel<true>" if c3 else "htm_run_frozen_kernel"
 
 
 def timed_replay(eng, vals, scores, a, steps, mode, chunk, gather, gathered, rank, world, device):

@@ -14,6 +14,9 @@ LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd.so")
 # diagnostic build with per-phase cycle stamps (tools/ only): HTM_AMD_STAMPS=1
 if os.environ.get("HTM_AMD_STAMPS") == "1":
     LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd_stamps.so")
+# A/B of two builds on one box (tools/ab_libs.py only): libhtm_amd_<variant>.so
+if os.environ.get("HTM_AMD_LIB_VARIANT"):
+    LIB_PATH = os.path.join(PKG_DIR, "libhtm_amd_%s.so" % os.environ["HTM_AMD_LIB_VARIANT"])
 # experiment builds (make variant ...; tools/ only)
 if os.environ.get("HTM_AMD_LIB"):
     LIB_PATH = os.path.join(PKG_DIR, os.environ["HTM_AMD_LIB"])

@@ -57,7 +57,6 @@ struct __attribute__((aligned(16))) TmSh {
     uint32_t cand[HTM_MAXACT];
     uint32_t newsrc[HTM_MAXSYN];
     uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
-    uint16_t lrn_pat[HTM_MAXPAT][HTM_MAXACT];
 #ifdef HTM_STAMPS
     uint64_t st_acc[HTM_NSTAMP], st_cnt[HTM_NSTAMP], st_last, st_start;
 #endif
@@ -72,6 +71,7 @@ struct Tm {
     float* colconf;
     uint32_t* flags;   // ncol bits
     uint32_t* U;       // union region
+    uint16_t (*lrnpat)[HTM_MAXACT];  // learn-state pattern ring (learning layouts only)
     // global, this stream
     uint32_t* meta;
     uint16_t* src;
@@ -108,7 +108,7 @@ enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
 // ---------------------------------------------------------------------------
 // LDS layout
 struct TmLayout {
-    size_t off_bm, off_conf, off_flags, off_U, total;
+    size_t off_lpat, off_bm, off_conf, off_flags, off_U, total;
     int nbm;
     size_t u_words;
 };
@@ -119,6 +119,8 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     TmLayout L;
     L.nbm = learn ? 7 : 3;
     size_t o = align16(sizeof(TmSh));
+    L.off_lpat = o;  // the learn-state pattern ring: learning only
+    if (learn) o = align16(o + (size_t)HTM_MAXPAT * HTM_MAXACT * 2);
     L.off_bm = o;
     o = align16(o + (size_t)L.nbm * c.cw * 4);
     L.off_conf = o;
@@ -1015,7 +1017,7 @@ __device__ __forceinline__ const uint16_t* inf_pat(Tm& t, int k) {
 }
 __device__ __forceinline__ int inf_len(Tm& t, int k) { return t.sh->inf_len[(t.sh->inf_head + k) % HTM_MAXPAT]; }
 __device__ __forceinline__ const uint16_t* lrn_pat(Tm& t, int k) {
-    return t.sh->lrn_pat[(t.sh->lrn_head + k) % HTM_MAXPAT];
+    return t.lrnpat[(t.sh->lrn_head + k) % HTM_MAXPAT];
 }
 __device__ __forceinline__ int lrn_len(Tm& t, int k) { return t.sh->lrn_len[(t.sh->lrn_head + k) % HTM_MAXPAT]; }
 
@@ -1841,7 +1843,7 @@ __device__ __forceinline__ void update_learning(Tm& t) {
     }
     __syncthreads();
     if (sh->ti[1] >= 0)
-        for (int a = threadIdx.x; a < sh->nA; a += TM_NT) sh->lrn_pat[sh->ti[1]][a] = sh->act[a];
+        for (int a = threadIdx.x; a < sh->nA; a += TM_NT) t.lrnpat[sh->ti[1]][a] = sh->act[a];
     __syncthreads();
     process_segment_updates(t, sh->act, sh->nA);
     if (threadIdx.x == 0) {
@@ -1966,6 +1968,7 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     t.colconf = reinterpret_cast<float*>(lds + L.off_conf);
     t.flags = reinterpret_cast<uint32_t*>(lds + L.off_flags);
     t.U = reinterpret_cast<uint32_t*>(lds + L.off_U);
+    t.lrnpat = LEARN ? reinterpret_cast<uint16_t(*)[HTM_MAXACT]>(lds + L.off_lpat) : nullptr;
     const size_t sc = (size_t)c.seg_cap;
     // model buffers: the stream's own, or the fleet's shared instance 0
     // (frozen inference writes only the segments' dutyCycle cache, with the
@@ -2088,7 +2091,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
             } else {
                 const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
                 if (a < sh->lrn_len[slot])
-                    sh->lrn_pat[slot][a] = gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a];
+                    t.lrnpat[slot][a] = gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a];
             }
         }
         if (threadIdx.x == 0) {
@@ -2181,7 +2184,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
                 gpat[sh->ti[0] * HTM_MAXACT + a] = sh->inf_pat[sh->ti[0]][a];
         if (LEARN && sh->ti[1] >= 0)
             for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
-                gpat[(HTM_MAXPAT + sh->ti[1]) * HTM_MAXACT + a] = sh->lrn_pat[sh->ti[1]][a];
+                gpat[(HTM_MAXPAT + sh->ti[1]) * HTM_MAXACT + a] = t.lrnpat[sh->ti[1]][a];
     } else {
         const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
         for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
@@ -2191,7 +2194,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
                 if (a < sh->inf_len[slot]) gpat[slot * HTM_MAXACT + a] = sh->inf_pat[slot][a];
             } else {
                 const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
-                if (a < sh->lrn_len[slot]) gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a] = sh->lrn_pat[slot][a];
+                if (a < sh->lrn_len[slot]) gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a] = t.lrnpat[slot][a];
             }
         }
     }

@@ -1,13 +1,27 @@
-"""Summarise a gpu_round.sh run into profiles/<tag>/: rocprof kernel stats,
-PMC FETCH_SIZE / WRITE_SIZE per kernel, and the HBM traffic per stream-step
-of the frozen inference kernel (the bench's dominant kernel).
+"""HBM traffic per dispatch from rocprofv3 --pmc passes, calibrated.
 
-FETCH_SIZE and WRITE_SIZE are in KB per dispatch.  Per MI355X_MICROARCH.md
-(HBM section) gfx950's FETCH_SIZE reports half the bytes of 16-byte-per-lane
-streaming reads, which is what the out-list block loads are, so it is
-doubled ("fetch_corrected"); the kernel also issues 4/8-byte gathers, for
-which the correction is uncalibrated -- the corrected figure is an upper
-estimate, the raw one a lower."""
+Usage: python tools/pmc_summary.py <run dir> <out dir> [--calib <calib dir> <calib bytes json>]
+
+<run dir> holds the rocprofv3 output directories of the passes over ONE
+command (tools/gpu_prof.sh):
+  pmc_rd/     TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
+  pmc_fetch/  FETCH_SIZE
+  pmc_wr/     WRITE_SIZE TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
+  prof/       --kernel-trace --stats (kernel_stats.csv is copied along)
+Counters are per dispatch; the median over the dispatches of each kernel is
+reported.  Read bytes are counted from the L2 memory-side read requests by
+size class, 32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B, write bytes
+as 64 x WRREQ_64B + 32 x (WRREQ - WRREQ_64B); FETCH_SIZE / WRITE_SIZE are
+reported beside them.  MI355X_MICROARCH.md (HBM section) calibrates
+FETCH_SIZE only for 16-byte-per-lane streaming reads (it reports half of
+them); --calib checks the request-size formula and FETCH_SIZE against the
+known bytes of tools/fetch_calib's access patterns (the widths the frozen TM
+kernel issues), and the verdict is written beside the numbers.
+
+Output <out dir>/pmc_summary.json: {"kernels": {name: {... ,
+"hbm_bytes_per_dispatch": B, "formula": "..."}}, "calibration": {...}} --
+the file bench.py --pmc-summary reads.
+"""
 import csv
 import json
 import os
@@ -15,39 +29,90 @@ import shutil
 import statistics
 import sys
 
-src, dst = sys.argv[1], sys.argv[2]
-streams = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
-# steps per dispatch of the frozen kernel: the PMC passes run one htm_run chunk
-# of 256 steps (gpu_round.sh); 1 for per-step (--mode step) passes
-steps = int(sys.argv[4]) if len(sys.argv) > 4 else 256
-os.makedirs(dst, exist_ok=True)
-out = {"source": src, "streams": streams, "steps_per_dispatch": steps, "kernels": {}}
-for name, cn in [("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")]:
-    path = os.path.join(src, name, "run_counter_collection.csv")
-    if not os.path.exists(path):
-        continue
-    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == cn]
-    per = {}
-    for r in rows:
-        per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
-    for k, v in per.items():
-        e = out["kernels"].setdefault(k, {})
-        e[cn] = {"dispatches": len(v), "median_kb": statistics.median(v), "mean_kb": sum(v) / len(v)}
-frozen = [k for k in out["kernels"] if "htm_run_frozen_kernel" in k or
-          ("<false, true>" in k and ("htm_run_kernel" in k or "tm_step_kernel" in k))]
-if frozen:
-    e = out["kernels"][frozen[0]]
-    f = e.get("FETCH_SIZE", {}).get("median_kb", 0.0) * 1024
-    w = e.get("WRITE_SIZE", {}).get("median_kb", 0.0) * 1024
-    out["frozen_kernel"] = frozen[0]
-    u = streams * steps
-    out["per_stream_step"] = {"fetch_raw": f / u, "fetch_corrected": 2 * f / u, "write": w / u,
-                              "traffic": (2 * f + w) / u}
-json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-ks = os.path.join(src, "prof", "run_kernel_stats.csv")
-if os.path.exists(ks):
-    shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))
-for f in ["bench.json", "prof_bench.json", "stamps.json", "gpu_tests.log"]:
-    if os.path.exists(os.path.join(src, f)):
-        shutil.copy(os.path.join(src, f), os.path.join(dst, f))
-print(json.dumps(out.get("per_stream_step"), indent=1))
+
+def load_pass(path):
+    """{kernel: {counter: [values per dispatch]}}"""
+    f = os.path.join(path, "run_counter_collection.csv")
+    out = {}
+    if not os.path.exists(f):
+        return out
+    for r in csv.DictReader(open(f)):
+        out.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return out
+
+
+def med(d, k, c):
+    v = d.get(k, {}).get(c)
+    return statistics.median(v) if v else None
+
+
+def summarise(run):
+    rd, fe, wr = (load_pass(os.path.join(run, p)) for p in ("pmc_rd", "pmc_fetch", "pmc_wr"))
+    kernels = {}
+    for k in set(rd) | set(fe) | set(wr):
+        e = {}
+        r32, r64, r128, rall = (med(rd, k, c) for c in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+                                                       "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_sum"))
+        w64, wall = med(wr, k, "TCC_EA0_WRREQ_64B_sum"), med(wr, k, "TCC_EA0_WRREQ_sum")
+        if None not in (r32, r64, r128):
+            e["read_bytes"] = 32 * r32 + 64 * r64 + 128 * r128
+            e["rdreq"] = {"all": rall, "32B": r32, "64B": r64, "128B": r128}
+        if None not in (w64, wall):
+            e["write_bytes"] = 64 * w64 + 32 * (wall - w64)
+            e["wrreq"] = {"all": wall, "64B": w64}
+        fs, ws = med(fe, k, "FETCH_SIZE"), med(wr, k, "WRITE_SIZE")
+        if fs is not None:
+            e["fetch_size_bytes"] = fs * 1024
+        if ws is not None:
+            e["write_size_bytes"] = ws * 1024
+        n = max(len(d.get(k, {}).get(c, [])) for d, c in ((rd, "TCC_EA0_RDREQ_sum"), (fe, "FETCH_SIZE"),
+                                                         (wr, "WRITE_SIZE")))
+        e["dispatches"] = n
+        if "read_bytes" in e and "write_bytes" in e:
+            e["hbm_bytes_per_dispatch"] = e["read_bytes"] + e["write_bytes"]
+            e["formula"] = ("median per dispatch of 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B + "
+                            "64*WRREQ_64B + 32*(WRREQ - WRREQ_64B) (TCC_EA0 memory-side requests)")
+        kernels[k] = e
+    return kernels
+
+
+def main():
+    run, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    out = {"source": run, "kernels": summarise(run)}
+    if "--calib" in sys.argv:
+        i = sys.argv.index("--calib")
+        cdir, cjson = sys.argv[i + 1], sys.argv[i + 2]
+        known = json.load(open(cjson))
+        ck = summarise(cdir)
+        cal = {}
+        for name, kb in known.items():
+            m = [v for k, v in ck.items() if k.startswith(name + "(") or k == name]
+            if not m:
+                continue
+            e = m[0]
+            row = {"known": kb}
+            if "read" in kb:
+                row["formula_over_known"] = round(e.get("read_bytes", 0) / kb["read"], 4)
+                row["fetch_size_over_known"] = round(e.get("fetch_size_bytes", 0) / kb["read"], 4)
+                row["rdreq"] = e.get("rdreq")
+            else:
+                row["formula_over_known"] = round(e.get("write_bytes", 0) / kb["write"], 4)
+                row["write_size_over_known"] = round(e.get("write_size_bytes", 0) / kb["write"], 4)
+                row["wrreq"] = e.get("wrreq")
+            cal[name] = row
+        out["calibration"] = {"source": cdir, "patterns": cal,
+                              "note": "random gathers move whole lines: their formula/known is the line "
+                                      "over-fetch of the pattern, not a counter error; streaming patterns "
+                                      "(stream16, stream4, runs16, wstream16) check the counters"}
+    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    ks = os.path.join(run, "prof", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))
+    top = {k: {x: v.get(x) for x in ("hbm_bytes_per_dispatch", "fetch_size_bytes", "write_size_bytes")}
+           for k, v in out["kernels"].items() if "htm_run" in k or "tm_step" in k}
+    print(json.dumps({"kernels": top, "calibration": out.get("calibration", {}).get("patterns")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
