@@ -319,6 +319,7 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.scr_q, uint32_t, S * (size_t)d.q_cap);
     ALLOC(e->tm.scr_q2, uint32_t, std::max(S * (size_t)d.q_cap, cap));
     ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
+    ALLOC(e->tm.colnz, uint32_t, S * ((size_t)d.nw + 1));
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
     // backtrack assist buffers (frozen lockstep launches): ~16 x 14 KB per
@@ -498,7 +499,13 @@ int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
 
 int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
-    if (opt == HTM_OPT_FROZEN_INDEX) e->use_frozen = value ? 1 : 0;
+    if (opt == HTM_OPT_FROZEN_INDEX) {
+        // a fleet's streams share the model's segment records: only the frozen
+        // index reads them race-free (the pool scan's dutyCycle() reads and
+        // writes the shared records)
+        if (!value && e->fleet) return htm_fail(HTM_E_INVALID, "fleet engines always run the frozen index");
+        e->use_frozen = value ? 1 : 0;
+    }
     else if (opt == HTM_OPT_KEEP_PREV) e->keep_prev = value ? 1 : 0;
     else if (opt == HTM_OPT_KEEP_OVERLAPS) e->keep_overlaps = value ? 1 : 0;
     else if (opt == HTM_OPT_PROFILE) {
@@ -887,6 +894,16 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
     return HTM_OK;
 }
 
+// The kernels write colConfidence back sparsely against a per-stream bitmap
+// of its nonzero columns (TmBufs::colnz); any host-side change of the TM
+// state marks the bitmaps stale, so the next write-back is dense.
+static int invalidate_colnz(htm_engine* e, void* stream) {
+    const size_t bytes = (size_t)e->n * ((size_t)e->dc.nw + 1) * 4;
+    if (hipMemsetAsync(e->tm.colnz, 0, bytes, (hipStream_t)stream) != hipSuccess)
+        return htm_fail(HTM_E_HIP, "colnz reset: %s", hipGetErrorString(hipGetLastError()));
+    return HTM_OK;
+}
+
 int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes) {
     if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
         return htm_fail(HTM_E_INVALID, "bad import arguments");
@@ -895,13 +912,13 @@ int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy((uint8_t*)r.base + r.per_stream * s0, h_src, r.per_stream * n, hipMemcpyHostToDevice));
     if (region >= HTM_ST_TM_HEADER) e->fx_valid = false;
-    return HTM_OK;
+    return invalidate_colnz(e, nullptr);
 }
 
 int htm_reset_tm(htm_engine* e, void* stream) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
     if (launch_tm_reset(e->dc, e->tm, e->n, (hipStream_t)stream)) return htm_fail(HTM_E_HIP, "reset launch");
-    return HTM_OK;
+    return invalidate_colnz(e, stream);
 }
 
 // Broadcast one stream's slice of a per-stream region into every other
@@ -945,6 +962,7 @@ int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     if (replicate_region((uint8_t*)e->sp.act, HTM_MAXACT * 2, src, e->n, st) ||
         replicate_region((uint8_t*)e->sp.nact, 4, src, e->n, st))
         return htm_fail(HTM_E_HIP, "replicate launch");
+    if (invalidate_colnz(e, stream)) return HTM_E_HIP;
     HIP_TRY(hipStreamSynchronize(st));
     e->fx_valid = false;
     return HTM_OK;

@@ -584,54 +584,75 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
 // predicted cells (rows path; the frozen pid path predicted them while
 // counting), the dutyCycle() each contributes, emit(k, slot, cell, dc).
 // Returns this thread's algorithmic bytes.
+// connected synapses of pool slot `slot` onto active cells (>= activationThreshold
+// predicts the segment's cell); adds the bytes read to nb
+__device__ __forceinline__ uint32_t seg_connected_activity(Tm& t, uint32_t slot, uint32_t nsyn, uint32_t& nb) {
+    nb += 4u + 16u * ((nsyn + 7u) / 8u);
+    const uint32_t cm = t.conn[slot];
+    const uint4* row = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
+    uint32_t n = 0;
+    for (int q = 0; q < 4; q++) {
+        if ((uint32_t)q * 8 >= nsyn) break;
+        uint4 v = row[q];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k2 = 0; k2 < 8; k2++) {
+            uint32_t j = q * 8 + k2;
+            uint32_t sid = (w[k2 >> 1] >> ((k2 & 1) * 16)) & 0xFFFFu;
+            if (j < nsyn && ((cm >> j) & 1u) && bm_get(t.infA, sid)) n++;
+        }
+    }
+    return n;
+}
+
 template <bool FROZEN, typename F>
 __device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     uint32_t nb = 0;
-    const bool fx_pid = FROZEN && t.np <= (uint32_t)c.fx_pcap;
-    for (uint32_t k = threadIdx.x; k < qn && fx_pid; k += TM_NT) {
+    // frozen: the cells the pid counters did not predict (more pids than
+    // fx_pcap) come from the segments' synapse rows
+    const bool rows = FROZEN && t.np > (uint32_t)c.fx_pcap;
+    for (uint32_t k = threadIdx.x; k < qn && FROZEN; k += TM_NT) {
         // frozen index: cell and the (frozen-iteration) dutyCycle of the
         // segment of rank q1[k].  The dutyCycle() state update is a store of
-        // the value it returns.
+        // the value it returns; the value read never comes from the pool's
+        // record, which streams sharing a model (fleet) may be refreshing.
         const uint32_t rank = t.q1[k];
         const uint2 rec = t.fxrec[rank];
+        const uint32_t cell = rec.x & 0xFFFFu;
         // the dutyCycle() state write stores the same value every time while
         // the iteration counter is frozen: only the first one after the index
         // build changes the record (FX_FRESH marks it done, or never needed)
+        uint32_t slot = ~0u;
+        if (!(rec.x & FX_FRESH) || rows) {
+            slot = t.fxrslot[rank];
+            nb += 4u;
+        }
         if (!(rec.x & FX_FRESH)) {
-            const uint32_t slot = t.fxrslot[rank];
             t.duty[(size_t)slot * 3 + 1] = rec.y;
             t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
             atomicOr(const_cast<uint32_t*>(&t.fxrec[rank].x), FX_FRESH);
-            nb += 12u;
+            nb += 8u;
         }
         nb += 8u;
-        emit(k, rank, rec.x & 0xFFFFu, __uint_as_float(rec.y));
-    }
-    for (uint32_t k = threadIdx.x; k < qn && !fx_pid; k += TM_NT) {
-        // q1 holds ranks (frozen) or pool slots (learning scan)
-        uint32_t slot = FROZEN ? t.fxrslot[t.q1[k]] : t.q1[k];
-        if (FROZEN) nb += 4u;
-        uint32_t m = t.meta[slot];
-        uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
-        // meta + conn + used source rows + duty-cycle record read and written
-        nb += 4u + 4u + 16u * ((nsyn + 7u) / 8u) + 12u + 8u;
-        uint32_t cm = t.conn[slot];
-        const uint4* row = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
-        uint32_t n = 0;
-        for (int q = 0; q < 4; q++) {
-            if ((uint32_t)q * 8 >= nsyn) break;
-            uint4 v = row[q];
-            uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k2 = 0; k2 < 8; k2++) {
-                uint32_t j = q * 8 + k2;
-                uint32_t sid = (w[k2 >> 1] >> ((k2 & 1) * 16)) & 0xFFFFu;
-                if (j < nsyn && ((cm >> j) & 1u) && bm_get(t.infA, sid)) n++;
-            }
+        if (rows) {
+            const uint32_t nsyn = meta_nsyn(t.meta[slot]);
+            if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
+                atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
+            nb += 4u;
         }
-        if (n >= (uint32_t)c.act_thr) atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
+        emit(k, rank, cell, __uint_as_float(rec.y));
+    }
+    for (uint32_t k = threadIdx.x; k < qn && !FROZEN; k += TM_NT) {
+        // learning scan: pool slots
+        const uint32_t slot = t.q1[k];
+        const uint32_t m = t.meta[slot];
+        const uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
+        // meta + conn + used source rows + duty-cycle record read and written
+        nb += 4u + 12u + 8u;
+        if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
+            atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
         emit(k, slot, cell, seg_dc_update(t.duty, slot, sh->lrn_iter, false));
     }
     return nb;
@@ -989,9 +1010,28 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
     return npcol;
 }
 
+// The confidences a frozen phase 2 computes matter only if its state is the
+// one the step keeps: P2_DISCARD -- a backtrack replay before the current
+// pattern (its phase 1 reads only the predicted cells); P2_IF_IN_SEQ -- the
+// step's own phase 2 or a replay's last one (kept exactly when in sequence,
+// otherwise a backtrack or the next start recomputes); P2_KEEP -- always.
+// Skipped confidence sums leave colConfidence zero.  The segments' dutyCycle()
+// state updates happen in every case, as in NuPIC.
+enum { P2_DISCARD = 0, P2_IF_IN_SEQ = 1, P2_KEEP = 2 };
+
+// frozen phase 2 whose confidences are discarded: the dutyCycle() state
+// updates of the qualifying segments only
+__device__ __forceinline__ void phase2_duty_only(Tm& t) {
+    const uint32_t qn = (uint32_t)t.sh->qn;
+    const uint32_t nb = phase2_pass1<true>(t, qn, [](uint32_t, uint32_t, uint32_t, float) {});
+    if (nb) atomicAdd(&t.sh->bytes, (unsigned long long)nb);
+    COUNT(t, SC_QN, qn);
+    COUNT(t, SC_P2, 1);
+}
+
 // _inferPhase2()
 template <bool FROZEN>
-__device__ __forceinline__ bool infer_phase2(Tm& t) {
+__device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
     TmSh* sh = t.sh;
     if (threadIdx.x == 0) {
         sh->st[0]++;
@@ -1008,6 +1048,14 @@ __device__ __forceinline__ bool infer_phase2(Tm& t) {
         sh->qn = t.c.q_cap;
     }
     __syncthreads();
+    if (FROZEN && need != P2_KEEP && t.np <= (uint32_t)t.c.fx_pcap) {
+        // the pid counters have predicted the cells: decide first
+        const bool inSeq = (double)count_predicted_cols(t) >= 0.5 * sh->avg_dens;
+        if (need == P2_IF_IN_SEQ && inSeq) (void)phase2_finish<FROZEN>(t);
+        else phase2_duty_only(t);
+        __syncthreads();
+        return inSeq;
+    }
     uint32_t npc = phase2_finish<FROZEN>(t);
     return (double)npc >= 0.5 * sh->avg_dens;
 }
@@ -1064,7 +1112,7 @@ __device__ __forceinline__ bool bt_replay(Tm& t, int start, int numPrev) {
         __syncthreads();
         inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
         if (!inSeq) break;
-        inSeq = infer_phase2<FROZEN>(t);
+        inSeq = infer_phase2<FROZEN>(t, off == numPrev - 1 ? P2_IF_IN_SEQ : P2_DISCARD);
         if (!inSeq) break;
     }
     return inSeq;
@@ -1185,27 +1233,37 @@ __device__ __forceinline__ void infer_backtrack_assisted(Tm& t, int numPrev, uin
     (void)cur;
 }
 
-// _inferBacktrack(activeColumns)
+// _inferBacktrack(activeColumns).  gprevP: infPredictedState(t-1) in HBM
+// when the step's state was loaded from there (first step of a run: the
+// write-back comes only at the end of the step), else null.  The replays
+// overwrite the LDS copy, so that one is the backup; otherwise a scratch
+// copy is kept.  NuPIC's saved candidate state is not copied: the loop stops
+// at the candidate, so the live state already is it; and with no candidate
+// the current pattern's phase 1 is recomputed from infP(t-1) instead of
+// restoring a saved infActiveState (same state, computed the same way).
 template <bool FROZEN>
-__device__ __forceinline__ void infer_backtrack(Tm& t) {
+__device__ __forceinline__ void infer_backtrack(Tm& t, const uint32_t* gprevP) {
     TmSh* sh = t.sh;
     const int cw = t.c.cw;
     const int numPrev = sh->n_inf_pat;
     if (numPrev <= 0) return;
     const int cur = numPrev - 1;
     if (threadIdx.x == 0) sh->st[1]++;
-    uint32_t* bkA = t.sbm;
-    uint32_t* bkP = t.sbm + cw;
-    uint32_t* cdA = t.sbm + 2 * cw;
-    uint32_t* cdP = t.sbm + 3 * cw;
-    wg_copy(bkA, t.infA, cw);
-    wg_copy(bkP, t.infP1, cw);
-    __syncthreads();
-    if (FROZEN && t.bt_epoch) {
-        infer_backtrack_assisted<FROZEN>(t, numPrev, bkA, bkP);
+    const bool assisted = FROZEN && t.bt_epoch;
+    const uint32_t* bkP = gprevP;
+    if (!bkP || assisted) {
+        wg_copy(t.sbm + cw, t.infP1, cw);
+        bkP = t.sbm + cw;
+    }
+    if (assisted) {
+        uint32_t* bkA = t.sbm;
+        wg_copy(bkA, t.infA, cw);
+        __syncthreads();
+        infer_backtrack_assisted<FROZEN>(t, numPrev, bkA, t.sbm + cw);
         STAMP(t, SB_BT);
         return;
     }
+    __syncthreads();
     uint32_t bad = 0;
     bool haveCand = false;
     int candStart = -1;
@@ -1218,7 +1276,7 @@ __device__ __forceinline__ void infer_backtrack(Tm& t) {
             STAMP(t, SB_BT);
             inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
             if (!inSeq) break;
-            inSeq = infer_phase2<FROZEN>(t);
+            inSeq = infer_phase2<FROZEN>(t, off == cur ? P2_IF_IN_SEQ : P2_DISCARD);
             if (!inSeq) break;
         }
         if (!inSeq) {
@@ -1227,22 +1285,13 @@ __device__ __forceinline__ void infer_backtrack(Tm& t) {
         }
         haveCand = true;
         candStart = start;
-        if (candStart == cur) break;
-        wg_copy(cdA, t.infA, cw);
-        wg_copy(cdP, t.infP, cw);
-        wg_copy(reinterpret_cast<uint32_t*>(t.sconf), reinterpret_cast<const uint32_t*>(t.colconf), t.c.ncol);
-        __syncthreads();
         break;
     }
+    wg_copy(t.infP1, bkP, cw);
+    __syncthreads();
     if (!haveCand) {
-        wg_copy(t.infA, bkA, cw);
-        __syncthreads();
+        (void)infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
         (void)infer_phase2<FROZEN>(t);
-    } else if (candStart != cur) {
-        wg_copy(t.infA, cdA, cw);
-        wg_copy(t.infP, cdP, cw);
-        wg_copy(reinterpret_cast<uint32_t*>(t.colconf), reinterpret_cast<const uint32_t*>(t.sconf), t.c.ncol);
-        __syncthreads();
     }
     if (threadIdx.x == 0) {
         int npop = 0;
@@ -1252,19 +1301,15 @@ __device__ __forceinline__ void infer_backtrack(Tm& t) {
         }
         sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
         sh->n_inf_pat -= npop;
-        // scratch traffic: backup out + in, candidate out + in
-        unsigned long long bb = 2ull * 4ull * cw + 4ull * cw + (haveCand ? 0ull : 4ull * cw);
-        if (haveCand && candStart != cur) bb += 2ull * (2ull * 4ull * cw + 4ull * t.c.ncol);
-        sh->bytes += bb;
+        // infP(t-1) backup: scratch out + in, or one read of the HBM state
+        sh->bytes += (gprevP ? 4ull : 8ull) * cw;
     }
-    wg_copy(t.infP1, bkP, cw);
-    __syncthreads();
     STAMP(t, SB_BT);
 }
 
 // _updateInferenceState(activeColumns)
 template <bool FROZEN>
-__device__ __forceinline__ void update_inference(Tm& t) {
+__device__ __forceinline__ void update_inference(Tm& t, const uint32_t* gprevP) {
     TmSh* sh = t.sh;
     if (threadIdx.x == 0) {
         if (t.c.max_inf_bt > 0) {
@@ -1286,11 +1331,12 @@ __device__ __forceinline__ void update_inference(Tm& t) {
     __syncthreads();
     bool inSeq = infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
     if (!inSeq) {
-        infer_backtrack<FROZEN>(t);
+        infer_backtrack<FROZEN>(t, gprevP);
         return;
     }
-    inSeq = infer_phase2<FROZEN>(t);
-    if (!inSeq) infer_backtrack<FROZEN>(t);
+    // with a pattern history, a phase 2 out of sequence is redone by the backtrack
+    inSeq = infer_phase2<FROZEN>(t, sh->n_inf_pat > 0 ? P2_IF_IN_SEQ : P2_KEEP);
+    if (!inSeq) infer_backtrack<FROZEN>(t, gprevP);
 }
 
 // ---------------------------------------------------------------------------
@@ -2006,6 +2052,89 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     t.bt_epoch = 0;
 }
 
+// Write the inference state back to HBM, touching only what changed:
+// infActiveState words that differ from HBM (the old words are loaded first,
+// their latency hidden behind the colConfidence bitmap), infPredictedState
+// words that differ from infP(t-1) (on the first step of a run the LDS copy
+// is what HBM holds), and colConfidence sparsely: gnz[0..nw) is the
+// nonzero-column bitmap of the dense HBM copy, gnz[nw] == 1 says it is valid
+// (the host clears it whenever it changes the state), so only the columns
+// nonzero before or now are written.  Uses t.flags (free after the TM step).
+// Returns the bytes this thread moved.  Contains barriers.
+__device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint32_t* gbm, float* gconf,
+                                                         uint32_t* gnz) {
+    const DevCfg& c = t.c;
+    constexpr int PER = 4;  // old infA words prefetched per thread (all of them up to 32,768 cells)
+    uint32_t olda[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int w = threadIdx.x + j * TM_NT;
+        olda[j] = w < c.cw ? gbm[w] : 0u;
+    }
+    uint32_t oldnz[(HTM_MAXNW + TM_NT - 1) / TM_NT];
+#pragma unroll
+    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
+        const int w = threadIdx.x + j * TM_NT;
+        oldnz[j] = w < c.nw ? gnz[w] : 0u;
+    }
+    const bool valid = gnz[c.nw] == 1u;
+    uint32_t* nzb = t.flags;  // the new bitmap
+    uint32_t* ozb = t.U;      // the old one (the union is free after the step)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
+        const int w = threadIdx.x + j * TM_NT;
+        if (w < c.nw) ozb[w] = oldnz[j];
+    }
+    // nonzero-column bitmap of the LDS colConfidence (ballots over 64 columns)
+    for (int col0 = wave_id() * 64; col0 < c.ncol; col0 += TM_NT) {
+        const int col = col0 + lane_id();
+        const uint64_t bal = __ballot(col < c.ncol && t.colconf[col] != 0.0f);
+        if (lane_id() == 0) {
+            nzb[col0 >> 5] = (uint32_t)bal;
+            if (col0 + 32 < c.ncol) nzb[(col0 >> 5) + 1] = (uint32_t)(bal >> 32);
+        }
+    }
+    __syncthreads();
+    uint32_t wb = 4u * (uint32_t)c.cw / TM_NT;  // old infA words read
+    for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
+        const uint32_t nb = (nzb[col >> 5] >> (col & 31)) & 1u;
+        const uint32_t ob = valid ? (ozb[col >> 5] >> (col & 31)) & 1u : 1u;
+        if (nb | ob) {
+            gconf[col] = t.colconf[col];
+            wb += 4;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
+        const int w = threadIdx.x + j * TM_NT;
+        if (w < c.nw && (!valid || oldnz[j] != nzb[w])) {
+            gnz[w] = nzb[w];
+            wb += 4;
+        }
+    }
+    if (threadIdx.x == 0 && !valid) gnz[c.nw] = 1u;
+    for (int j = 0; threadIdx.x + j * TM_NT < (uint32_t)c.cw; j++) {
+        const int w = threadIdx.x + j * TM_NT;
+        uint32_t o = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++)
+            if (i == j) o = olda[i];
+        if (j >= PER) o = gbm[w];
+        const uint32_t v = t.infA[w];
+        if (o != v) {
+            gbm[w] = v;
+            wb += 4;
+        }
+        const uint32_t p = t.infP[w];
+        if (!first || t.infP1[w] != p) {
+            gbm[c.cw + w] = p;
+            wb += 4;
+        }
+    }
+    return wb;
+}
+
 template <bool LEARN, bool FROZEN>
 // first / last: the step opens / closes a run of steps by this workgroup.
 // Between them the stream's TM state (cell bitmaps, colConfidence, header,
@@ -2140,7 +2269,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     STAMP(t, SB_LOAD);
     if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) compact_pool(t);
     // ---- BacktrackingTM.compute(input, learn, infer=True)
-    update_inference<FROZEN>(t);
+    update_inference<FROZEN>(t, first ? gbm + c.cw : nullptr);
     STAMP(t, SB_BT);
     if (LEARN) update_learning(t);
     STAMP(t, SB_LEARN);
@@ -2169,13 +2298,14 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
 #endif
         return;
     }
-    wg_copy(gbm, t.infA, c.cw);
-    wg_copy(gbm + c.cw, t.infP, c.cw);
+    // cell bitmaps: only the words that changed.  infA's previous words are
+    // re-read from HBM; on the first step of a run infP1 holds what HBM holds
+    uint32_t wb = write_back_inference(t, first, gbm, gconf, b.colnz + (size_t)s * (c.nw + 1));
     if (LEARN) {
         wg_copy(gbm + 2 * c.cw, t.lrnA, c.cw);
         wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
+        if (threadIdx.x == 0) wb += 8 * c.cw;
     }
-    wg_copy(reinterpret_cast<uint32_t*>(gconf), reinterpret_cast<const uint32_t*>(t.colconf), c.ncol);
     // patterns: a single step changes only the slot it pushed (pops move
     // the heads); a run of steps writes back every live slot
     if (first) {
@@ -2198,15 +2328,18 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
             }
         }
     }
+    wb = wg_sum(sh, wb);
     if (threadIdx.x == 0) {
-        // bitmaps out, colConfidence out (dense), pushed patterns, score
-        sh->bytes += (LEARN ? 4ull : 2ull) * 4ull * c.cw + 4ull * c.ncol + (LEARN ? 4ull : 2ull) * sh->nA + 4ull;
+        // bitmaps out (changed words; infA's old words read), colConfidence
+        // out (sparse), nonzero-column map, pushed patterns, score
+        sh->bytes += wb + (LEARN ? 4ull : 2ull) * sh->nA + 4ull;
         hdr->stat_bytes += sh->bytes_acc + sh->bytes;
     }
-    if (threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
+    // the RNG moves only when learning; a single step changes one ring slot's length
+    if (LEARN && threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
     if (threadIdx.x < HTM_MAXPAT) {
-        hdr->inf_pat_len[threadIdx.x] = sh->inf_len[threadIdx.x];
-        hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
+        if (!first || (int)threadIdx.x == sh->ti[0]) hdr->inf_pat_len[threadIdx.x] = sh->inf_len[threadIdx.x];
+        if (LEARN && (!first || (int)threadIdx.x == sh->ti[1])) hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
     }
     if (threadIdx.x == 0) {
         hdr->avg_input_density = sh->avg_dens;

@@ -26,14 +26,17 @@ def replicas(rt, model, n):
     return eng
 
 
-@pytest.mark.parametrize("frozen", [True, False])
-def test_fleet_equals_replicated_engines(rt, model, traces, frozen):
+@pytest.mark.parametrize("pid_lists", [True, False])
+def test_fleet_equals_replicated_engines(rt, model, traces, pid_lists, monkeypatch):
+    """pid_lists False: the frozen index without pid lists (HTM_FX_PID=0, read
+    at engine creation), phase 2 reading the qualifying segments' synapse rows."""
     n, T = 16, 120
+    if not pid_lists:
+        monkeypatch.setenv("HTM_FX_PID", "0")
     rep = replicas(rt, model, n)
     fl = rt.HTMEngine.fleet(model, n, q_capacity=4096)
+    monkeypatch.delenv("HTM_FX_PID", raising=False)
     assert fl.is_fleet and fl.device_bytes() < rep.device_bytes() / 4
-    for e in (rep, fl):
-        e.use_frozen_index(frozen)
     rng = np.random.default_rng(17)
     base = np.asarray(traces["test"][:T], np.float64)
     vals = np.clip(base[:, None] + rng.integers(-3, 4, size=(T, n)), 0, 100)
@@ -66,5 +69,7 @@ def test_fleet_refuses_learning_and_save(rt, model, tmp_path):
     fl = rt.HTMEngine.fleet(model, 4)
     with pytest.raises(rt.HtmError):
         fl.set_learning(True, False)
+    with pytest.raises(rt.HtmError):  # the pool scan would race on the shared segment records
+        fl.use_frozen_index(False)
     with pytest.raises(rt.HtmError):
         fl.save(str(tmp_path / "f.htm"))
