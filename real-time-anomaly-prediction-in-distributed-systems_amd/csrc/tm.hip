@@ -431,34 +431,63 @@ __device__ __forceinline__ void fx_qualify(const uint32_t* cnt, uint32_t nbytes,
 // sweeps a contiguous run of quads; one workgroup scan places the runs), so
 // the qualifying list comes out in rank = (cell, creation) order.  Counters
 // never exceed 32 (see fx_qualify).  Contains barriers: call uniformly.
+// 16-bit hit mask of one counter quad: bit 4j+i set when byte i of word j
+// is >= thr (add = 0x01010101 * (128 - thr); counters never exceed 32)
+__device__ __forceinline__ uint32_t fx_quad_hits(uint4 x, uint32_t add) {
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    uint32_t h = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t m = (w[j] + add) & 0x80808080u;
+        h |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
+    }
+    return h;
+}
+
+#ifndef FX_CQ
+#define FX_CQ 16  // counter quads one thread sweeps (W <= 16 x 16 x TM_NT bytes)
+#endif
+
 __device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t nquads, uint32_t thr, uint32_t base,
                                                    TmSh* sh, uint32_t* dst, uint32_t qcap) {
     const uint32_t add = 0x01010101u * (128u - thr);
     const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
-    const uint32_t per = (nquads + TM_NT - 1) / TM_NT;
+    const uint32_t per = (nquads + TM_NT - 1) / TM_NT;  // <= FX_CQ (fx_win <= 64512)
     const uint32_t q0 = threadIdx.x * per;
-    const uint32_t q1 = q0 + per < nquads ? q0 + per : nquads;
+    // one sweep: every quad of the thread's run loaded at once, its hits kept
+    // as 16-bit masks (two per register)
+    uint32_t hm[FX_CQ / 2];
     uint32_t mine = 0;
-    for (uint32_t q = q0; q < q1; q++) {
-        const uint4 x = c4[q];
-        mine += __popc((x.x + add) & 0x80808080u) + __popc((x.y + add) & 0x80808080u) +
-                __popc((x.z + add) & 0x80808080u) + __popc((x.w + add) & 0x80808080u);
-    }
-    const uint32_t qn0 = (uint32_t)sh->qn;  // thread 0 updates it only after the barrier below
-    uint32_t tot;
-    uint32_t pos = qn0 + wg_excl_scan(sh, mine, &tot);
-    for (uint32_t q = q0; q < q1 && mine; q++) {
-        const uint4 x = c4[q];
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            for (uint32_t m = (w[j] + add) & 0x80808080u; m; m &= m - 1) {
-                if (pos < qcap) dst[pos] = base + 16 * q + 4 * j + ((__ffs(m) - 1) >> 3);
+    for (int i = 0; i < FX_CQ; i++) {
+        uint32_t h = 0;
+        if ((uint32_t)i < per && q0 + i < nquads) h = fx_quad_hits(c4[q0 + i], add);
+        if (i & 1) hm[i >> 1] |= h << 16;
+        else hm[i >> 1] = h;
+        mine += __popc(h);
+    }
+    // exclusive prefix over the workgroup in thread order (one barrier)
+    const uint32_t qn0 = (uint32_t)sh->qn;  // thread 0 updates it only after the barrier
+    const uint32_t incl = wave_incl_scan(mine);
+    if (lane_id() == 63) sh->red[TM_NWAVES + wave_id()] = incl;
+    __syncthreads();
+    uint32_t pos = qn0 + incl - mine, tot = 0;
+#pragma unroll
+    for (int v = 0; v < TM_NWAVES; v++) {
+        const uint32_t x = sh->red[TM_NWAVES + v];
+        if (v < (int)wave_id()) pos += x;
+        tot += x;
+    }
+    if (mine) {
+#pragma unroll
+        for (int i = 0; i < FX_CQ; i++) {
+            for (uint32_t m = (hm[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; m; m &= m - 1) {
+                const uint32_t b = __ffs(m) - 1;  // 4 * word + byte
+                if (pos < qcap) dst[pos] = base + 16 * (q0 + i) + b;
                 pos++;
             }
         }
     }
-    __syncthreads();
     if (threadIdx.x == 0) sh->qn = (int32_t)(qn0 + tot);
 }
 
