@@ -8,14 +8,18 @@ from tests/golden/model1_traces.npz).  Inputs are synthetic, resident in HBM:
     cpu[s,t] = clip(trace[(t + 97 s) mod 2324] + d[s,t], 0, 100)
 trace = TestingData.txt cpu column, d uniform integer in {-2..2} from
 numpy PCG64(seed=724).  A step = one network.run(1) of every stream
-(encoder -> SP -> TM -> raw anomaly).  `value` times the K steps as htm_run
-replay chunks (the reference's offline replay of recorded metrics,
-ModelTesting.py over TestingData.txt, batched: each stream steps through a
-chunk without waiting for the others); the same engine is then also timed
-in lockstep (one htm_step per step, every stream waits for the slowest) and
-reported as `lockstep`.  N>1 GPUs: weak scaling, streams sharded by rank,
-RCCL gather of every step's anomaly scores to rank 0 (the SLO alerting
-path) in one collective per htm_run chunk, overlapped with the next chunk.
+(encoder -> SP -> TM -> raw anomaly).  `value` times the K steps in LOCKSTEP
+(the headline, north_star's real-time stepping: one htm_step per step, every
+stream advances one record and waits for the slowest); the same engine is
+then timed in run mode (`run_mode`: the K steps as htm_run replay chunks,
+each stream stepping through a chunk without waiting for the others -- the
+reference's offline replay of recorded metrics, ModelTesting.py over
+TestingData.txt, batched).  N>1 GPUs: weak scaling, streams sharded by
+rank, RCCL gather of every step's anomaly scores to rank 0 (the SLO
+alerting path).  roofline.traffic: at N=1, before the timed run, bench.py
+runs the same workload under rocprofv3 once per counter pass (child
+processes) and reads the HBM bytes per launch of the dominant kernel from
+them (tools/pmc_summary.py; --no-pmc skips, --pmc-summary reuses passes).
 
 Run:  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S]
 """
@@ -282,7 +286,9 @@ def main():
                          "beside the lockstep headline; config 2: 2324, config 4: 64, config 3: 0 = skip)")
     ap.add_argument("--pmc-summary", default=None,
                     help="JSON from tools/pmc_summary.py over rocprofv3 --pmc passes of this same command "
-                         "(same gpurun call): fills roofline.traffic; otherwise traffic is null")
+                         "(same gpurun call): fills roofline.traffic")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the counter passes bench.py runs itself (N=1) to fill roofline.traffic")
     args = ap.parse_args()
     c3, c4, c5 = args.config == 3, args.config == 4, args.config == 5
     if c5:
@@ -304,6 +310,13 @@ def main():
         args.other_steps = 0 if c3 else 64 if c4 else 2324
     if c4:
         args.chunk = min(args.chunk, int(os.environ.get("HTM_C4_MAX_CHUNK", "64")))
+    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.pmc_summary and not args.no_pmc and not c5
+            and not os.environ.get("HTM_BENCH_PMC_CHILD")):
+        # before this process touches the GPU: the HBM counter passes, each a
+        # short run of this same command under rocprofv3 in a child process
+        args.pmc_summary, pmc_note = self_pmc_passes(args)
+    else:
+        pmc_note = None
 
     import torch
     import torch.distributed as dist
@@ -405,7 +418,7 @@ def main():
         avg_ms = prof["tm_ms"] / launches
         per_launch = tm_bytes / launches
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = None, None
+        traffic, tsrc = None, pmc_note
         if args.pmc_summary:
             # HBM bytes per launch measured by rocprofv3 --pmc passes of THIS command
             # (tools/pmc_summary.py, run in the same gpurun call; corrections there)
@@ -416,7 +429,8 @@ def main():
             k = ks[0] if ks else None
             if k:
                 traffic = int(k["hbm_bytes_per_dispatch"])
-                tsrc = f"{args.pmc_summary}: {k.get('formula', '')}"
+                tsrc = (f"rocprofv3 --pmc passes of this command ({args.pmc_summary}): {k.get('formula', '')}; "
+                        "calibrated on tools/fetch_calib (profiles/r02_final/pmc_summary.json)")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
@@ -455,6 +469,51 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+# rocprofv3 --pmc passes (one run each; TCC block: 4 counters, FETCH_SIZE costs 3,
+# WRITE_SIZE 2): L2 memory-side requests by size, FETCH_SIZE, writes
+PMC_PASSES = {
+    "pmc_rd": ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum"],
+    "pmc_fetch": ["FETCH_SIZE"],
+    "pmc_wr": ["WRITE_SIZE", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"],
+}
+
+
+def self_pmc_passes(args, steps=128):
+    """Run this benchmark's workload (same config/streams, `steps` timed steps,
+    the same launch shape as the timed region) under rocprofv3 once per
+    counter pass and summarise them (tools/pmc_summary.py).  Returns
+    (summary path, note); (None, reason) when the passes cannot run."""
+    import shutil
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found: traffic not measured"
+    out = tempfile.mkdtemp(prefix="htm_pmc_", dir="/tmp")
+    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
+             "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode]
+    for k in ("streams", "seg_capacity", "chunk", "run_unit"):
+        v = getattr(args, k)
+        if v is not None:
+            child += ["--" + k.replace("_", "-"), str(v)]
+    env = dict(os.environ, TMPDIR="/tmp", HTM_BENCH_PMC_CHILD="1")
+    for name, counters in PMC_PASSES.items():
+        cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", os.path.join(out, "run", name), "-o", "run",
+               "--", *child]
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=420)
+        except subprocess.TimeoutExpired:
+            return None, "rocprofv3 pass %s timed out: traffic not measured" % name
+        if r.returncode != 0:
+            return None, "rocprofv3 pass %s failed (rc %d): traffic not measured" % (name, r.returncode)
+    import pmc_summary
+    kernels = pmc_summary.summarise(os.path.join(out, "run"))
+    path = os.path.join(out, "pmc_summary.json")
+    json.dump({"source": out, "kernels": kernels}, open(path, "w"), indent=1)
+    return path, None
 
 
 def kernel_name(c3, c4, fused):

@@ -51,8 +51,9 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t qn;
     int32_t ncand;
     int32_t ti[8];
+    int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
     float tf[4];
-    uint32_t red[2 * TM_NWAVES];
+    uint32_t red[3 * TM_NWAVES];
     uint16_t act[HTM_MAXACT];
     uint32_t cand[HTM_MAXACT];
     uint32_t newsrc[HTM_MAXSYN];
@@ -183,6 +184,10 @@ __device__ __forceinline__ uint32_t wg_sum(TmSh* sh, uint32_t v) {
     __syncthreads();
     return t;
 }
+// The same with one barrier, through its own slots of sh->red: callers must
+// have passed another barrier since the previous call read them.
+__device__ __forceinline__ uint32_t wg_excl_scan1(TmSh* sh, uint32_t v, uint32_t* total);
+
 // exclusive prefix over the workgroup in thread order; *total gets the sum
 __device__ __forceinline__ uint32_t wg_excl_scan(TmSh* sh, uint32_t v, uint32_t* total) {
     uint32_t incl = wave_incl_scan(v);
@@ -196,6 +201,21 @@ __device__ __forceinline__ uint32_t wg_excl_scan(TmSh* sh, uint32_t v, uint32_t*
         tot += sh->red[w];
     }
     __syncthreads();
+    *total = tot;
+    return base + incl - v;
+}
+
+__device__ __forceinline__ uint32_t wg_excl_scan1(TmSh* sh, uint32_t v, uint32_t* total) {
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane_id() == 63) sh->red[2 * TM_NWAVES + wave_id()] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < TM_NWAVES; w++) {
+        const uint32_t x = sh->red[2 * TM_NWAVES + w];
+        if (w < (int)wave_id()) base += x;
+        tot += x;
+    }
     *total = tot;
     return base + incl - v;
 }
@@ -569,7 +589,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         }
         if (w + 1 < (int)nw) load_offsets(w + 1);
         uint32_t B;
-        uint32_t pos = wg_excl_scan(sh, lsum, &B);
+        uint32_t pos = wg_excl_scan1(sh, lsum, &B);
         for (uint32_t j = 0; j < per; j++) {
             const uint32_t k = k0 + j;
             if (k >= na) break;
@@ -840,7 +860,9 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
             const uint32_t col = col_at(k);
             if (k == 0 || col_at(k - 1) != col) t.colconf[col] /= tot;
         }
-    const uint32_t npcol = count_predicted_cols(t);  // (barriers)
+    // numPredictedCols: counted by infer_phase2 before the tail when the pid
+    // counters predicted the cells; from the rows read in pass 1 otherwise
+    const uint32_t npcol = t.np > (uint32_t)c.fx_pcap ? count_predicted_cols(t) : (uint32_t)sh->npc_known;
     STAMP(t, SB_FIN2);
     return npcol;
 }
@@ -1065,6 +1087,7 @@ __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
     if (threadIdx.x == 0) {
         sh->st[0]++;
         sh->qn = 0;
+        sh->npc_known = -1;
     }
     wg_clear(t.infP, t.c.cw);
     wg_clear(reinterpret_cast<uint32_t*>(t.colconf), t.c.ncol);
@@ -1077,11 +1100,17 @@ __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
         sh->qn = t.c.q_cap;
     }
     __syncthreads();
-    if (FROZEN && need != P2_KEEP && t.np <= (uint32_t)t.c.fx_pcap) {
+    if (FROZEN && t.np <= (uint32_t)t.c.fx_pcap) {
         // the pid counters have predicted the cells: decide first
-        const bool inSeq = (double)count_predicted_cols(t) >= 0.5 * sh->avg_dens;
-        if (need == P2_IF_IN_SEQ && inSeq) (void)phase2_finish<FROZEN>(t);
-        else phase2_duty_only(t);
+        const uint32_t npc = count_predicted_cols(t);
+        const bool inSeq = (double)npc >= 0.5 * sh->avg_dens;
+        if (need == P2_KEEP || (need == P2_IF_IN_SEQ && inSeq)) {
+            if (threadIdx.x == 0) sh->npc_known = (int32_t)npc;
+            __syncthreads();
+            (void)phase2_finish<FROZEN>(t);
+        } else {
+            phase2_duty_only(t);
+        }
         __syncthreads();
         return inSeq;
     }
