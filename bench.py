@@ -267,8 +267,10 @@ def main():
     ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: 2324, config 3: 240)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config 2: 64, config 3: 16)")
     ap.add_argument("--streams", type=int, default=None,
-                    help="streams per GPU (config 2: 1024; config 3: 40960 -- 65,536 x 256 learning steps "
-                         "needs ~380 GB of float32 state, more than one MI355X holds; see DESIGN.md)")
+                    help="streams per GPU (config 2: 1024; config 3: 65536, BASELINE.json configs[2])")
+    ap.add_argument("--sp-perm-rows", type=int, default=None,
+                    help="paged SP permanences: pool rows per stream (config 3: 800 -- fresh streams touch "
+                         "~25-30%% of their 2048 columns in 256 steps; 0 = dense)")
     ap.add_argument("--seg-capacity", type=int, default=None, help="segment slots per stream")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
@@ -301,7 +303,9 @@ def main():
     if args.warmup is None:
         args.warmup = 16 if (c3 or c4) else 64
     if args.streams is None:
-        args.streams = 40960 if c3 else 131072 if c4 else 1024
+        args.streams = 65536 if c3 else 131072 if c4 else 1024
+    if args.sp_perm_rows is None:
+        args.sp_perm_rows = 800 if c3 else 0
     if args.seg_capacity is None:
         args.seg_capacity = 10240 if c3 else 72 * 1024
     if args.chunk is None:
@@ -342,7 +346,7 @@ def main():
     if c3:
         # fresh per-stream init (seeds 2045 + global stream index), learning on
         cfg = rt.default_config(seg_capacity=args.seg_capacity, upd_capacity=512, seed_stride=1,
-                                sp_seed=2045 + s0, tm_seed=2045 + s0)
+                                sp_seed=2045 + s0, tm_seed=2045 + s0, sp_perm_rows=args.sp_perm_rows)
         t0 = time.time()
         eng = rt.HTMEngine(S, config=cfg, device=local)
         torch.cuda.synchronize()
@@ -455,6 +459,8 @@ def main():
                    "streams_per_gpu": S, "total_streams": n_total, "columns": 2048, "cells_per_column": 12,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
                    "segments_after": int(c1["seg_live"] // S) if c3 else None,
+                   "sp_perm_rows": ({"per_stream": args.sp_perm_rows, "used_per_stream": round(eng.sp_perm_rows_used() / S, 1),
+                                     "device_gb": round(eng.device_bytes() / 1e9, 1)} if c3 else None),
                    ("init_s" if c3 else "train_s"): round(train_s, 2),
                    "model_distribution": model_dist,
                    "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL gather of scores" if world > 1 else "")},
@@ -495,12 +501,13 @@ def self_pmc_passes(args, steps=128):
     out = tempfile.mkdtemp(prefix="htm_pmc_", dir="/tmp")
     child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
              "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode]
-    for k in ("streams", "seg_capacity", "chunk", "run_unit"):
+    for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows"):
         v = getattr(args, k)
         if v is not None:
             child += ["--" + k.replace("_", "-"), str(v)]
     env = dict(os.environ, TMPDIR="/tmp", HTM_BENCH_PMC_CHILD="1")
     for name, counters in PMC_PASSES.items():
+        t0 = time.time()
         cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", os.path.join(out, "run", name), "-o", "run",
                "--", *child]
         try:
@@ -509,6 +516,7 @@ def self_pmc_passes(args, steps=128):
             return None, "rocprofv3 pass %s timed out: traffic not measured" % name
         if r.returncode != 0:
             return None, "rocprofv3 pass %s failed (rc %d): traffic not measured" % (name, r.returncode)
+        print(f"bench: counter pass {name} done in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     import pmc_summary
     kernels = pmc_summary.summarise(os.path.join(out, "run"))
     path = os.path.join(out, "pmc_summary.json")

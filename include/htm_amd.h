@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HTM_ABI_VERSION 2
+#define HTM_ABI_VERSION 3
 
 /* error codes */
 #define HTM_OK 0
@@ -108,6 +108,18 @@ typedef struct {
      * stay shared.  Zero (htm_default_config) = the shared range. */
     double field_minval[4];
     double field_maxval[4];
+    /* SP permanence storage.  0 (htm_default_config): dense, ncol rows of
+     * n_potential floats per stream.  > 0: paged -- one pool of
+     * n_streams * sp_perm_rows rows shared by all streams; a column gets a
+     * row on its first permanence change (adaptSynapses_ / bumpUpWeakColumns_),
+     * until then its permanences are the NuPIC initial values, regenerated on
+     * the GPU from per-stream nupic::Random checkpoints (one per 8 columns).
+     * Fresh learning streams touch ~25-30 % of their columns in 256 steps,
+     * so config 3 (65,536 learning streams, BASELINE.json configs[2]) fits one
+     * GPU.  Results are identical to the dense layout; an exhausted pool sets
+     * error flag 32 (htm_status: HTM_E_CAPACITY, results invalid). */
+    int32_t sp_perm_rows;
+    int32_t reserved0;           /* 0 */
 } htm_config;
 
 typedef struct htm_engine htm_engine;
@@ -217,6 +229,13 @@ size_t htm_output_bytes(const htm_engine* eng, int32_t which);
 #define HTM_ST_TM_CELL_NSEG 14 /* uint8 [ncells] segments per cell */
 #define HTM_ST_TM_PATTERNS 15  /* uint16 [inf 16 + lrn 16][64] pattern history rings */
 #define HTM_ST_TM_UPDATES 16   /* htm_tm_update [upd_capacity] */
+#define HTM_ST_SP_PERM_CKPT 17 /* paged engines (sp_perm_rows > 0) only, else 0 bytes:
+                                  uint32 [ncol/8][64] nupic::Random checkpoints of the SP
+                                  initialisation, one per 8 columns (the initial permanences
+                                  of columns without a pool row).  Importing it re-bases the
+                                  stream (its permanences keep their values); importing 0
+                                  bytes keeps the stream's own. */
+#define HTM_ST_COUNT 17
 size_t htm_state_bytes(const htm_engine* eng, int32_t region);
 int htm_export_state(htm_engine* eng, int32_t region, int32_t stream_begin, int32_t n,
                      void* h_dst, size_t bytes);
@@ -283,6 +302,9 @@ int32_t htm_n_streams(const htm_engine* eng);
 int htm_get_config(const htm_engine* eng, htm_config* out);
 /* Bytes of device memory held by the engine. */
 size_t htm_device_bytes(const htm_engine* eng);
+/* Paged SP permanences: pool rows handed out so far (synchronises; 0 for a
+ * dense engine).  Rows never return to the pool. */
+uint64_t htm_sp_perm_rows_used(htm_engine* eng);
 /* 1 when the frozen-TM forward index (used while TM learning is off) is
  * current. */
 int32_t htm_frozen_index_valid(const htm_engine* eng);

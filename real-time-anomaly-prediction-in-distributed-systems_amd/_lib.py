@@ -31,7 +31,9 @@ HTM_E_STATE = -5
 
 OUT = dict(active_columns=1, prev_pred_columns=2, inf_active=3, inf_predicted=4, lrn_active=5,
            lrn_predicted=6, col_confidence=7, tm_output=8, sp_overlaps=9)
-ST = dict(sp_connT=1, sp_potmask=2, sp_perm=3, sp_duty=4, sp_scalars=5, tm_header=6, tm_bitmaps=7,
+# sp_perm_ckpt first: a paged engine imports its permanences against the
+# initial values of the checkpoints they came with (HTM_ST_SP_PERM_CKPT)
+ST = dict(sp_perm_ckpt=17, sp_connT=1, sp_potmask=2, sp_perm=3, sp_duty=4, sp_scalars=5, tm_header=6, tm_bitmaps=7,
           tm_colconf=8, tm_seg_meta=9, tm_seg_src=10, tm_seg_perm=11, tm_seg_conn=12, tm_seg_duty=13,
           tm_cell_nseg=14, tm_patterns=15, tm_updates=16)
 OPT_FROZEN_INDEX = 1
@@ -67,6 +69,7 @@ class HtmConfig(ctypes.Structure):
         ("seg_capacity", ctypes.c_int32), ("upd_capacity", ctypes.c_int32), ("seed_stride", ctypes.c_int32),
         ("sdr_bits", ctypes.c_int32),
         ("field_minval", ctypes.c_double * 4), ("field_maxval", ctypes.c_double * 4),
+        ("sp_perm_rows", ctypes.c_int32), ("reserved0", ctypes.c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -104,7 +107,7 @@ EXPORTED = [
     "htm_default_config", "htm_create", "htm_destroy", "htm_set_learning", "htm_set_option", "htm_status",
     "htm_step", "htm_run", "htm_step_sdr", "htm_run_sdr", "htm_get_output", "htm_output_bytes", "htm_state_bytes", "htm_export_state",
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
-    "htm_get_config", "htm_device_bytes", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
+    "htm_get_config", "htm_device_bytes", "htm_sp_perm_rows_used", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
     "htm_profile_read", "htm_counters", "htm_debug_stamps",
     "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats", "htm_create_fleet", "htm_is_fleet",
     "htm_likelihood_create", "htm_likelihood_destroy", "htm_likelihood_step",
@@ -170,6 +173,8 @@ def lib():
     L.htm_get_config.argtypes = [vp, P(HtmConfig)]
     L.htm_device_bytes.argtypes = [vp]
     L.htm_device_bytes.restype = sz
+    L.htm_sp_perm_rows_used.argtypes = [vp]
+    L.htm_sp_perm_rows_used.restype = ctypes.c_uint64
     L.htm_frozen_index_valid.argtypes = [vp]
     L.htm_frozen_index_valid.restype = i32
     L.htm_last_error.restype = ctypes.c_char_p

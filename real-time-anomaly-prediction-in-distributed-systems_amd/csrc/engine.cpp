@@ -69,7 +69,7 @@ struct htm_engine {
     bool fx_valid = false;
     size_t fx_cap = 0;
     uint64_t* d_counts = nullptr;
-    Region regions[17];
+    Region regions[HTM_ST_COUNT + 1];
     int32_t profile = 0;
     std::vector<hipEvent_t> ev_pool;
     std::vector<int32_t> ev_steps;  // steps covered by each profiled event triple
@@ -181,6 +181,13 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.nw = c.sp_columns / 32;
     // mapPotential_: WrappingNeighborhood(radius = inputWidth) covers all inputs
     d.n_potential = (int32_t)roundf((float)d.nin * c.sp_potential_pct);
+    // paged permanences: a shared pool of n * sp_perm_rows rows (row index u32)
+    if (c.sp_perm_rows < 0 || (uint64_t)c.sp_perm_rows * (uint64_t)n >= 0xFFFFFFFFull)
+        return htm_fail(HTM_E_INVALID, "sp_perm_rows must be >= 0 and n_streams * sp_perm_rows < 2^32");
+    d.sp_paged = c.sp_perm_rows > 0 ? 1 : 0;
+    d.n_ckpt = (c.sp_columns + SP_CKPT_COLS - 1) / SP_CKPT_COLS;
+    d.pool_stride = (int32_t)round_up((size_t)d.n_potential, 32);
+    d.pool_rows = (uint64_t)c.sp_perm_rows * (uint64_t)n;
     // inhibitColumns_: inhibitionRadius = max(columnDimensions) (global)
     uint32_t area = (uint32_t)powf((float)(2 * c.sp_columns + 1), 1.0f);
     if (area > (uint32_t)c.sp_columns) area = (uint32_t)c.sp_columns;
@@ -296,7 +303,17 @@ static int allocate(htm_engine* e) {
     ALLOC(e->wq, uint32_t, S + 1);
     ALLOC(e->sp.connT, uint32_t, M * d.nin_pad * d.nw);
     ALLOC(e->sp.potmask, uint32_t, M * d.ncol * (d.nin_pad / 32));
-    ALLOC(e->sp.perm, float, M * d.ncol * d.n_potential);
+    if (d.sp_paged) {
+        e->sp.perm = nullptr;
+        ALLOC(e->sp.prow, uint32_t, M * d.ncol);
+        HIP_TRY(hipMemset(e->sp.prow, 0xFF, M * d.ncol * 4));  // SP_ROW_NONE: initial values
+        ALLOC(e->sp.pool, float, (size_t)d.pool_rows * d.pool_stride);
+        ALLOC(e->sp.pool_next, unsigned long long, 1);
+        ALLOC(e->sp.ckpt, uint32_t, M * d.n_ckpt * SP_CKPT_WORDS);
+    } else {
+        ALLOC(e->sp.perm, float, M * d.ncol * d.n_potential);
+    }
+    ALLOC(e->sp.err, uint32_t, S);
     ALLOC(e->sp.duty, float, M * 2 * d.ncol);
     ALLOC(e->sp.scalars, uint32_t, S * 4);
     ALLOC(e->sp.act, uint16_t, S * HTM_MAXACT);
@@ -350,10 +367,12 @@ static int allocate(htm_engine* e) {
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
     Region* r = e->regions;
-    for (int i = 0; i < 17; i++) r[i] = Region{nullptr, 0, false};
+    for (int i = 0; i <= HTM_ST_COUNT; i++) r[i] = Region{nullptr, 0, false};
     r[HTM_ST_SP_CONNT] = {e->sp.connT, (size_t)d.nin_pad * d.nw * 4, true};
     r[HTM_ST_SP_POTMASK] = {e->sp.potmask, (size_t)d.ncol * (d.nin_pad / 32) * 4, true};
+    // paged engines: no base (export/import convert to and from the dense layout)
     r[HTM_ST_SP_PERM] = {e->sp.perm, (size_t)d.ncol * d.n_potential * 4, true};
+    r[HTM_ST_SP_PERM_CKPT] = {e->sp.ckpt, d.sp_paged ? (size_t)d.n_ckpt * SP_CKPT_WORDS * 4 : 0, true};
     r[HTM_ST_SP_DUTY] = {e->sp.duty, (size_t)2 * d.ncol * 4, true};
     r[HTM_ST_SP_SCALARS] = {e->sp.scalars, 16, false};
     r[HTM_ST_TM_HEADER] = {e->tm.hdr, sizeof(htm_tm_header), false};
@@ -735,6 +754,9 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; k++) out8[k] = 0;
+    std::vector<uint32_t> spe((size_t)e->n);
+    HIP_TRY(hipMemcpy(spe.data(), e->sp.err, spe.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t x : spe) out8[7] |= x;
     for (const auto& x : h) {
         out8[0] += x.stat_bytes;
         out8[1] += x.stat_inf_phase2;
@@ -875,7 +897,7 @@ int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void
 }
 
 size_t htm_state_bytes(const htm_engine* e, int32_t region) {
-    if (!e || region < 1 || region > 16) return 0;
+    if (!e || region < 1 || region > HTM_ST_COUNT) return 0;
     return e->regions[region].per_stream;
 }
 
@@ -884,12 +906,98 @@ static int32_t region_count(const htm_engine* e, int32_t region) {
     return e->regions[region].model ? e->nm : e->n;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Paged SP permanences <-> the dense HTM_ST_SP_PERM layout, a chunk of
+// streams at a time through a device staging buffer (<= 256 MiB).
+static size_t paged_chunk(const htm_engine* e) {
+    const size_t per = e->regions[HTM_ST_SP_PERM].per_stream;
+    return std::max<size_t>(1, ((size_t)256 << 20) / per);
+}
+
+// streams [s0, s0+n) into h_dst (host) or d_dst (device), dense
+static int paged_perm_export(htm_engine* e, int32_t s0, int32_t n, void* h_dst, float* d_dst) {
+    const size_t per = e->regions[HTM_ST_SP_PERM].per_stream;
+    if (d_dst) {
+        if (launch_sp_perm_export(e->dc, e->sp, d_dst, s0, n, nullptr)) return htm_fail(HTM_E_HIP, "perm export launch");
+        HIP_TRY(hipDeviceSynchronize());
+        return HTM_OK;
+    }
+    const int32_t chunk = (int32_t)std::min<size_t>((size_t)n, paged_chunk(e));
+    float* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, per * chunk));
+    int rc = HTM_OK;
+    for (int32_t k = 0; k < n && !rc; k += chunk) {
+        const int32_t m = std::min(chunk, n - k);
+        if (launch_sp_perm_export(e->dc, e->sp, tmp, s0 + k, m, nullptr)) rc = htm_fail(HTM_E_HIP, "perm export launch");
+        else if (hipMemcpy((uint8_t*)h_dst + per * k, tmp, per * m, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = htm_fail(HTM_E_HIP, "perm export copy: %s", hipGetErrorString(hipGetLastError()));
+    }
+    (void)hipFree(tmp);
+    return rc;
+}
+
+// dense rows from h_src (host) or d_src (device, d_stride floats between
+// streams: 0 = the same row set for every stream) into streams [s0, s0+n)
+static int paged_perm_import(htm_engine* e, int32_t s0, int32_t n, const void* h_src, const float* d_src,
+                             size_t d_stride) {
+    const size_t per = e->regions[HTM_ST_SP_PERM].per_stream;
+    if (d_src) {
+        if (launch_sp_perm_import(e->dc, e->sp, d_src, d_stride, s0, n, nullptr)) return htm_fail(HTM_E_HIP, "perm import launch");
+        HIP_TRY(hipDeviceSynchronize());
+        return HTM_OK;
+    }
+    const int32_t chunk = (int32_t)std::min<size_t>((size_t)n, paged_chunk(e));
+    float* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, per * chunk));
+    int rc = HTM_OK;
+    for (int32_t k = 0; k < n && !rc; k += chunk) {
+        const int32_t m = std::min(chunk, n - k);
+        if (hipMemcpy(tmp, (const uint8_t*)h_src + per * k, per * m, hipMemcpyHostToDevice) != hipSuccess)
+            rc = htm_fail(HTM_E_HIP, "perm import copy: %s", hipGetErrorString(hipGetLastError()));
+        else if (launch_sp_perm_import(e->dc, e->sp, tmp, per / 4, s0 + k, m, nullptr) ||
+                 hipDeviceSynchronize() != hipSuccess)
+            rc = htm_fail(HTM_E_HIP, "perm import launch");
+    }
+    (void)hipFree(tmp);
+    return rc;
+}
+
+// New checkpoints or potential masks (what the initial values of columns
+// without a row are replayed from) for streams [s0, s0+n): their permanences
+// keep their values -- exported against the old initial values, re-imported
+// against the new.
+static int paged_rebase_import(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src) {
+    const size_t per = e->regions[HTM_ST_SP_PERM].per_stream;
+    const size_t cper = e->regions[region].per_stream;
+    uint8_t* base = (uint8_t*)e->regions[region].base;
+    const int32_t chunk = (int32_t)std::min<size_t>((size_t)n, paged_chunk(e));
+    float* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, per * chunk));
+    int rc = HTM_OK;
+    for (int32_t k = 0; k < n && !rc; k += chunk) {
+        const int32_t m = std::min(chunk, n - k);
+        rc = paged_perm_export(e, s0 + k, m, nullptr, tmp);
+        if (!rc && hipMemcpy(base + cper * (s0 + k), (const uint8_t*)h_src + cper * k, cper * m,
+                             hipMemcpyHostToDevice) != hipSuccess)
+            rc = htm_fail(HTM_E_HIP, "region %d import copy", region);
+        if (!rc) rc = paged_perm_import(e, s0 + k, m, nullptr, tmp, per / 4);
+    }
+    (void)hipFree(tmp);
+    return rc;
+}
+
+extern "C" {
+
 int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void* h_dst, size_t bytes) {
-    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
+    if (!e || region < 1 || region > HTM_ST_COUNT || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
         return htm_fail(HTM_E_INVALID, "bad export arguments");
     const Region& r = e->regions[region];
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "export buffer too small");
     HIP_TRY(hipDeviceSynchronize());
+    if (r.per_stream == 0) return HTM_OK;
+    if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_export(e, s0, n, h_dst, nullptr);
     HIP_TRY(hipMemcpy(h_dst, (uint8_t*)r.base + r.per_stream * s0, r.per_stream * n, hipMemcpyDeviceToHost));
     return HTM_OK;
 }
@@ -904,15 +1012,27 @@ static int invalidate_colnz(htm_engine* e, void* stream) {
     return HTM_OK;
 }
 
-int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes) {
-    if (!e || region < 1 || region > 16 || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
+// rebase = false: plain copies of the checkpoints / potential masks (htm_load,
+// whose fresh engine holds no permanences yet)
+static int import_region(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes,
+                         bool rebase) {
+    if (!e || region < 1 || region > HTM_ST_COUNT || s0 < 0 || n < 1 || s0 + n > region_count(e, region))
         return htm_fail(HTM_E_INVALID, "bad import arguments");
     const Region& r = e->regions[region];
+    // no checkpoints (an export of a dense engine): the streams keep their own
+    if (region == HTM_ST_SP_PERM_CKPT && (bytes == 0 || r.per_stream == 0)) return HTM_OK;
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "import buffer too small");
     HIP_TRY(hipDeviceSynchronize());
+    if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_import(e, s0, n, h_src, nullptr, 0);
+    if (rebase && e->dc.sp_paged && (region == HTM_ST_SP_PERM_CKPT || region == HTM_ST_SP_POTMASK))
+        return paged_rebase_import(e, region, s0, n, h_src);
     HIP_TRY(hipMemcpy((uint8_t*)r.base + r.per_stream * s0, h_src, r.per_stream * n, hipMemcpyHostToDevice));
     if (region >= HTM_ST_TM_HEADER) e->fx_valid = false;
     return invalidate_colnz(e, nullptr);
+}
+
+int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const void* h_src, size_t bytes) {
+    return import_region(e, region, s0, n, h_src, bytes, true);
 }
 
 int htm_reset_tm(htm_engine* e, void* stream) {
@@ -951,12 +1071,23 @@ static int replicate_region(uint8_t* base, size_t per, int32_t src, int32_t n, h
 int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     if (!e || src < 0 || src >= e->n) return htm_fail(HTM_E_INVALID, "bad source stream");
     hipStream_t st = (hipStream_t)stream;
-    for (int id = 1; id <= 16; id++) {
+    for (int id = 1; id <= HTM_ST_COUNT; id++) {
         const Region& r = e->regions[id];
-        if (!r.base) continue;
+        if (!r.base || !r.per_stream) continue;
         const int32_t cnt = region_count(e, id);
         if (cnt < 2) continue;
         if (replicate_region((uint8_t*)r.base, r.per_stream, src, cnt, st)) return htm_fail(HTM_E_HIP, "replicate launch");
+    }
+    if (e->dc.sp_paged && e->nm > 1) {
+        // the source's permanences (dense, once) imported into every stream,
+        // whose checkpoints (the initial values) are the source's now
+        HIP_TRY(hipStreamSynchronize(st));
+        float* tmp = nullptr;
+        HIP_TRY(hipMalloc(&tmp, e->regions[HTM_ST_SP_PERM].per_stream));
+        int rc = paged_perm_export(e, src, 1, nullptr, tmp);
+        if (!rc) rc = paged_perm_import(e, 0, e->n, nullptr, tmp, 0);
+        (void)hipFree(tmp);
+        if (rc) return rc;
     }
     // SP active list of the last step too (the TM reads it)
     if (replicate_region((uint8_t*)e->sp.act, HTM_MAXACT * 2, src, e->n, st) ||
@@ -978,12 +1109,21 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
     HIP_TRY(hipSetDevice(model->device));
     HIP_TRY(hipDeviceSynchronize());
     htm_engine* e = nullptr;
-    int r = create_uninit(&model->cfg, n_streams, device, &e, q_capacity);
+    htm_config fcfg = model->cfg;
+    fcfg.sp_perm_rows = 0;  // the fleet's one SP instance is dense (never learns)
+    int r = create_uninit(&fcfg, n_streams, device, &e, q_capacity);
     if (r) return r;
     // model regions -> the shared instance, per-stream regions -> stream 0 (then every stream)
-    for (int id = 1; id <= 16 && !r; id++) {
+    for (int id = 1; id <= HTM_ST_COUNT && !r; id++) {
         const Region& src = model->regions[id];
         const Region& dst = e->regions[id];
+        if (id == HTM_ST_SP_PERM_CKPT) continue;
+        if (id == HTM_ST_SP_PERM && model->dc.sp_paged) {
+            std::vector<uint8_t> buf(src.per_stream);
+            r = htm_export_state(const_cast<htm_engine*>(model), id, model_stream, 1, buf.data(), buf.size());
+            if (!r) r = htm_import_state(e, id, 0, 1, buf.data(), buf.size());
+            continue;
+        }
         if (!src.base || !dst.base || src.per_stream != dst.per_stream) {
             r = htm_fail(HTM_E_STATE, "region %d layout differs", id);
             break;
@@ -1018,6 +1158,15 @@ int htm_get_config(const htm_engine* e, htm_config* out) {
 
 size_t htm_device_bytes(const htm_engine* e) { return e ? e->bytes + e->fx_cap * 16 : 0; }
 
+uint64_t htm_sp_perm_rows_used(htm_engine* e) {
+    if (!e || !e->dc.sp_paged) return 0;
+    unsigned long long x = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(&x, e->sp.pool_next, sizeof(x), hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    return std::min<unsigned long long>(x, e->dc.pool_rows);
+}
+
 int32_t htm_frozen_index_valid(const htm_engine* e) { return e && e->fx_valid ? 1 : 0; }
 
 const char* htm_last_error(void) { return g_err.c_str(); }
@@ -1030,14 +1179,23 @@ int htm_status(htm_engine* e) {
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> spe((size_t)e->n);
+    HIP_TRY(hipMemcpy(spe.data(), e->sp.err, spe.size() * 4, hipMemcpyDeviceToHost));
     for (int s = 0; s < e->n; s++) {
+        if (spe[s] & SP_ERR_POOL)
+            return htm_fail(HTM_E_CAPACITY, "stream %d error flag 0x20: SP permanence row pool exhausted -- updates "
+                            "were dropped, results invalid; raise sp_perm_rows", s);
         if (h[s].error) return htm_fail(HTM_E_CAPACITY, "stream %d error flags 0x%x (1: segment pool full -- new segments were dropped, raise seg_capacity; 2: segment-update queue full; 4: >1 learn-predicted cell in a column; 8: learn-active cell list overflow; 16: qualifying-segment list overflow, results invalid -- raise q_capacity)", s, h[s].error);
     }
     return HTM_OK;
 }
 
 // ---------------------------------------------------------------------------
-// save / load: "HTMAMD01", abi, config, n, learning flags, then regions
+// save / load: "HTMAMD01", abi, config, n, learning flags, then regions --
+// the SP checkpoints first, so a paged engine's permanences are imported
+// against the initial values they were exported with
+static int save_order(int k) { return k == 0 ? HTM_ST_SP_PERM_CKPT : k; }
+
 int htm_save(htm_engine* e, const char* path) {
     if (!e || !path) return htm_fail(HTM_E_INVALID, "bad arguments");
     if (e->fleet) return htm_fail(HTM_E_STATE, "fleet engines are not saved: save the model engine they were built from");
@@ -1049,7 +1207,8 @@ int htm_save(htm_engine* e, const char* path) {
               std::fwrite(&e->cfg, sizeof(htm_config), 1, f) == 1 && std::fwrite(&e->n, 4, 1, f) == 1 &&
               std::fwrite(&e->sp_learn, 4, 1, f) == 1 && std::fwrite(&e->tm_learn, 4, 1, f) == 1;
     std::vector<uint8_t> buf;
-    for (int id = 1; ok && id <= 16; id++) {
+    for (int k = 0; ok && k < HTM_ST_COUNT; k++) {
+        const int id = save_order(k);
         const Region& r = e->regions[id];
         uint64_t nb = (uint64_t)r.per_stream * e->n;
         buf.resize(nb);
@@ -1085,7 +1244,8 @@ int htm_load(const char* path, int32_t device, htm_engine** out) {
         return r;
     }
     std::vector<uint8_t> buf;
-    for (int k = 1; ok && k <= 16; k++) {
+    for (int i = 0; ok && i < HTM_ST_COUNT; i++) {
+        const int k = save_order(i);
         int32_t rid;
         uint64_t nb;
         ok = std::fread(&rid, 4, 1, f) == 1 && std::fread(&nb, 8, 1, f) == 1 && rid == k &&
@@ -1093,7 +1253,7 @@ int htm_load(const char* path, int32_t device, htm_engine** out) {
         if (!ok) break;
         buf.resize(nb);
         ok = std::fread(buf.data(), 1, nb, f) == nb;
-        if (ok && htm_import_state(e, k, 0, n, buf.data(), nb)) ok = false;
+        if (ok && import_region(e, k, 0, n, buf.data(), nb, false)) ok = false;
     }
     std::fclose(f);
     if (!ok) {

@@ -63,7 +63,18 @@ struct DevCfg {
     int32_t shared_model;                 // fleet: every stream reads model instance 0 (SP + TM frozen)
     int32_t q_cap;                        // per-stream capacity of the qualifying-segment scratch lists
     int32_t sdr_in;                       // the SP reads an external input SDR of nin bits (no encoder)
+    // paged SP permanences (htm_config.sp_perm_rows > 0)
+    int32_t sp_paged;                     // 1: rows from SpBufs::pool on first change, else init values
+    int32_t n_ckpt;                       // nupic::Random checkpoints per stream (ncol / SP_CKPT_COLS)
+    int32_t pool_stride;                  // floats per pool row: n_potential rounded up to 128 B
+    int32_t pad0;
+    uint64_t pool_rows;                   // rows in SpBufs::pool
 };
+
+#define SP_CKPT_COLS 8      // columns per SP-initialisation checkpoint (paged permanences)
+#define SP_CKPT_WORDS 64    // words per checkpoint: st[31], idx, pending draws buf[31], pad
+#define SP_ROW_NONE 0xFFFFFFFFu
+#define SP_ERR_POOL 32u     // error flag: paged SP row pool exhausted (results invalid)
 
 // instance of the model buffers (SP permanences/connections, TM segment
 // pool, frozen index) stream s reads: its own, or the fleet's shared one
@@ -80,6 +91,12 @@ struct SpBufs {
     uint32_t* nact;     // [S]
     int32_t* overlaps;  // [S][ncol]
     uint64_t* seeds;    // [S] SP seed per stream
+    // paged permanences (DevCfg::sp_paged; perm is null then)
+    uint32_t* prow;     // [S][ncol] pool row of the column, SP_ROW_NONE: initial values
+    float* pool;        // [pool_rows][pool_stride]
+    unsigned long long* pool_next;  // [1] rows handed out
+    uint32_t* ckpt;     // [S][n_ckpt][SP_CKPT_WORDS] RNG state at columns 0, 8, 16, ... of sp_init
+    uint32_t* err;      // [S] SP error flags (SP_ERR_POOL)
 };
 
 struct TmBufs {
@@ -330,6 +347,9 @@ int htm_fail(int code, const char* fmt, ...);
 
 // host launch wrappers (defined in sp.hip / tm.hip)
 int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st);
+int launch_sp_perm_export(const DevCfg& c, const SpBufs& b, float* dst, int s0, int m, hipStream_t st);
+int launch_sp_perm_import(const DevCfg& c, const SpBufs& b, const float* src, size_t src_stride, int s0, int m,
+                          hipStream_t st);
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                    hipStream_t st);
 int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,

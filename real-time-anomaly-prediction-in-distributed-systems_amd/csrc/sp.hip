@@ -30,16 +30,7 @@
 // rows are built in the lane's LDS, stored column-major, and a second kernel
 // transposes the connected rows into the input-major bitmap the overlap reads.
 
-// 31 draws starting at phase 0 (draw index k = 0 mod 31): state and outputs
-__device__ __forceinline__ void rng_block(uint32_t (&st)[31], uint32_t* out) {
-#pragma unroll
-    for (int j = 0; j < 31; j++) {
-        const int f = (3 + j) % 31;
-        st[f] += st[j];
-        out[j] = (st[f] >> 1) & 0x7fffffffu;
-    }
-}
-
+// (rng_block, the 31-draw generator step, is in sp_dev.h)
 __device__ __forceinline__ void rng_seed_reg(uint32_t (&st)[31], uint64_t seed) {
     int32_t x = (int32_t)(seed % 2147483646ull + 1ull);
     st[0] = (uint32_t)x;
@@ -95,14 +86,19 @@ __global__ void sp_init_kernel(DevCfg c, SpBufs b, uint32_t* connC, int s0, int 
     const int nin = c.nin;
     uint32_t* pot = b.potmask + (size_t)s * c.ncol * pw;
     uint32_t* cc = connC + (size_t)(s - s0) * c.ncol * pw;
-    float* perm = b.perm + (size_t)s * c.ncol * c.n_potential;
-    const float span = 1.0f - c.sp_conn;  // synPermMax_ - synPermConnected_
-    const float conn = c.sp_conn;
-    const float ratio = (float)nin / (float)c.ncol;
+    float* perm = c.sp_paged ? nullptr : b.perm + (size_t)s * c.ncol * c.n_potential;
     for (int col = 0; col < c.ncol; col++) {
+        if (c.sp_paged && col % SP_CKPT_COLS == 0) {
+            // paged permanences: the generator state at the group's first
+            // column (state, hand-out index, the generated block)
+            uint32_t* ck = b.ckpt + ((size_t)s * c.n_ckpt + (size_t)(col / SP_CKPT_COLS)) * SP_CKPT_WORDS;
+#pragma unroll
+            for (int j = 0; j < 31; j++) ck[j] = g.st[j];
+            ck[31] = (uint32_t)g.idx;
+            for (int j = 0; j < 31; j++) ck[32 + j] = g.buf[j];
+        }
         for (int w = 0; w < pw; w++) prow[w] = crow[w] = 0u;
-        const float coord = (float)(((double)col + 0.5) * (double)ratio);
-        const int32_t center = (int32_t)floorf(coord);
+        const int32_t center = sp_column_center(c, col);
         // WrappingNeighborhood(center, radius = nin) order + Knuth selection sampling
         const uint32_t count = (uint32_t)nin;
         const uint32_t k = (uint32_t)c.n_potential;
@@ -121,21 +117,11 @@ __global__ void sp_init_kernel(DevCfg c, SpBufs b, uint32_t* connC, int s0, int 
         for (int w = 0; w < pw; w++) {
             for (uint32_t x = prow[w]; x; x &= x - 1) {
                 const int i = w * 32 + __ffs(x) - 1;
-                float p;
-                if (g.real64() <= 0.5) {
-                    p = conn + (float)((double)span * g.real64());
-                } else {
-                    p = conn * (float)g.real64();
-                }
-                p = (float)((double)(int32_t)(p * 100000.0f) / 100000.0);
-                p = p < c.sp_trim ? 0.0f : p;
-                // raisePermanencesToThreshold_: clip [0,1] (stimulus threshold 0 never loops)
-                p = p > 1.0f ? 1.0f : p;
-                p = p < 0.0f ? 0.0f : p;
-                const bool isconn = p >= c.sp_conn_thr;
-                p = p > 1.0f ? 1.0f : p;
-                p = p < c.sp_trim ? 0.0f : p;
-                pr[rank++] = p;
+                const uint32_t r0 = g.raw(), r1 = g.raw(), r2 = g.raw(), r3 = g.raw();
+                bool isconn;
+                const float p = sp_init_value(c, r0, r1, r2, r3, isconn);
+                if (!c.sp_paged) pr[rank] = p;
+                rank++;
                 if (isconn) crow[i >> 5] |= 1u << (i & 31);
             }
         }
@@ -209,6 +195,85 @@ int launch_sp_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st) {
     }
     (void)hipFree(connC);
     return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Paged SP permanences (DevCfg::sp_paged): the host-visible region
+// HTM_ST_SP_PERM keeps its dense layout [ncol][n_potential]; these kernels
+// convert between it and (pool rows + initial values replayed from the
+// checkpoints).  Export: one lane per (stream, 8-column group) writes the
+// initial values of the group's columns that have no row, then one wave per
+// (stream, column) copies the pool rows.  Import: one lane per (stream,
+// group) replays the initial values and gives a row to every column that
+// differs from them (or already has one) -- so a stream imported from its own
+// export holds no more rows than before.
+
+__global__ void sp_perm_export_init_kernel(DevCfg c, SpBufs b, float* dst, int s0, int m) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)m * c.n_ckpt) return;
+    const int sl = (int)(t / c.n_ckpt), g = (int)(t % c.n_ckpt), s = s0 + sl;
+    const int lo = g * SP_CKPT_COLS, hi = min(lo + SP_CKPT_COLS, c.ncol) - 1;
+    float* d = dst + (size_t)sl * c.ncol * c.n_potential;
+    const uint32_t* map = b.prow + (size_t)s * c.ncol;
+    sp_replay_init(sp_init_cfg(c, b), s, lo, hi, [&](int col, int k, float p) {
+        if (map[col] == SP_ROW_NONE) d[(size_t)col * c.n_potential + k] = p;
+    });
+}
+
+__global__ void sp_perm_export_rows_kernel(DevCfg c, SpBufs b, float* dst, int s0, int m) {
+    const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= (size_t)m * c.ncol) return;
+    const int sl = (int)(w / c.ncol), col = (int)(w % c.ncol);
+    const uint32_t r = b.prow[(size_t)(s0 + sl) * c.ncol + col];
+    if (r == SP_ROW_NONE) return;
+    const float* src = b.pool + (size_t)r * c.pool_stride;
+    float* d = dst + ((size_t)sl * c.ncol + col) * c.n_potential;
+    for (int k = lane_id(); k < c.n_potential; k += 64) d[k] = src[k];
+}
+
+__global__ void sp_perm_import_kernel(DevCfg c, SpBufs b, const float* src, size_t src_stride, int s0, int m) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)m * c.n_ckpt) return;
+    const int sl = (int)(t / c.n_ckpt), g = (int)(t % c.n_ckpt), s = s0 + sl;
+    const int lo = g * SP_CKPT_COLS, hi = min(lo + SP_CKPT_COLS, c.ncol) - 1;
+    const float* in = src + (size_t)sl * src_stride;
+    uint32_t* map = b.prow + (size_t)s * c.ncol;
+    uint32_t differ = 0;  // bit k: column lo + k differs from its initial values
+    sp_replay_init(sp_init_cfg(c, b), s, lo, hi, [&](int col, int k, float p) {
+        if (__float_as_uint(in[(size_t)col * c.n_potential + k]) != __float_as_uint(p)) differ |= 1u << (col - lo);
+    });
+    for (int col = lo; col <= hi; col++) {
+        uint32_t r = map[col];
+        if (r == SP_ROW_NONE && !((differ >> (col - lo)) & 1u)) continue;
+        if (r == SP_ROW_NONE) {
+            const unsigned long long x = atomicAdd(b.pool_next, 1ull);
+            if (x >= c.pool_rows) {
+                atomicOr(&b.err[s], SP_ERR_POOL);
+                continue;
+            }
+            r = (uint32_t)x;
+            map[col] = r;
+        }
+        float* row = b.pool + (size_t)r * c.pool_stride;
+        const float* x = in + (size_t)col * c.n_potential;
+        for (int k = 0; k < c.n_potential; k++) row[k] = x[k];
+    }
+}
+
+int launch_sp_perm_export(const DevCfg& c, const SpBufs& b, float* dst, int s0, int m, hipStream_t st) {
+    const size_t lanes = (size_t)m * c.n_ckpt;
+    hipLaunchKernelGGL(sp_perm_export_init_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st, c, b, dst, s0, m);
+    const size_t waves = (size_t)m * c.ncol;
+    hipLaunchKernelGGL(sp_perm_export_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, c, b, dst, s0, m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_sp_perm_import(const DevCfg& c, const SpBufs& b, const float* src, size_t src_stride, int s0, int m,
+                          hipStream_t st) {
+    const size_t lanes = (size_t)m * c.n_ckpt;
+    hipLaunchKernelGGL(sp_perm_import_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st, c, b, src,
+                       src_stride, s0, m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------------------

@@ -165,6 +165,191 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     }
 }
 
+// ---------------------------------------------------------------------------
+// SpatialPooler initialisation draws (nupic::Random, SURVEY.md Appendix A.2;
+// oracle/htm_oracle.c sp_init).  Shared by sp_init_kernel (sp.hip) and the
+// regeneration of a column's initial permanences for paged engines.
+
+// 31 draws starting at phase 0 (draw index k = 0 mod 31): state and outputs
+__device__ __forceinline__ void rng_block(uint32_t (&st)[31], uint32_t* out) {
+#pragma unroll
+    for (int j = 0; j < 31; j++) {
+        const int f = (3 + j) % 31;
+        st[f] += st[j];
+        out[j] = (st[f] >> 1) & 0x7fffffffu;
+    }
+}
+
+// What replaying the initialisation draws needs (a few scalars, so the cold
+// out-of-line replay of a fused kernel receives them in registers)
+struct SpInitCfg {
+    int32_t nin, nin_pad, ncol, n_potential, n_ckpt;
+    float sp_conn, sp_trim, sp_conn_thr;
+    const uint32_t* potmask;
+    const uint32_t* ckpt;
+};
+__device__ __forceinline__ SpInitCfg sp_init_cfg(const DevCfg& c, const SpBufs& b) {
+    return SpInitCfg{c.nin, c.nin_pad, c.ncol, c.n_potential, c.n_ckpt, c.sp_conn, c.sp_trim, c.sp_conn_thr,
+                     b.potmask, b.ckpt};
+}
+
+// mapColumn_: the centre input of column col (1-D, potentialRadius = nin)
+template <class C>
+__device__ __forceinline__ int32_t sp_column_center(const C& c, int col) {
+    const float ratio = (float)c.nin / (float)c.ncol;
+    const float coord = (float)(((double)col + 0.5) * (double)ratio);
+    return (int32_t)floorf(coord);
+}
+
+// Random::getReal64() of two raw draws (getUInt64(2^48), never rejected)
+__device__ __forceinline__ double sp_real64(uint32_t lo, uint32_t hi) {
+    return (double)(((uint64_t)lo | ((uint64_t)hi << 32)) & ((1ull << 48) - 1ull)) * (1.0 / 281474976710656.0);
+}
+
+// initPermanence_ of one potential synapse from its four draws (connected
+// with probability 0.5: synPermConnected + span * u, else synPermConnected *
+// u; 5-digit truncation; trim), then updatePermanencesForColumn_(raise)'s
+// clips (stimulusThreshold 0 never loops).  isconn: >= synPermConnected - eps.
+template <class C>
+__device__ __forceinline__ float sp_init_value(const C& c, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
+                                               bool& isconn) {
+    const float span = 1.0f - c.sp_conn;  // synPermMax_ - synPermConnected_
+    float p;
+    if (sp_real64(r0, r1) <= 0.5) p = c.sp_conn + (float)((double)span * sp_real64(r2, r3));
+    else p = c.sp_conn * (float)sp_real64(r2, r3);
+    p = (float)((double)(int32_t)(p * 100000.0f) / 100000.0);
+    p = p < c.sp_trim ? 0.0f : p;
+    p = p > 1.0f ? 1.0f : p;
+    p = p < 0.0f ? 0.0f : p;
+    isconn = p >= c.sp_conn_thr;
+    p = p > 1.0f ? 1.0f : p;
+    p = p < c.sp_trim ? 0.0f : p;
+    return p;
+}
+
+// Draws the potential-pool sampling of column col consumed: the selection
+// walks inputs in WrappingNeighborhood order from the centre and stops once
+// n_potential are chosen, so it made (wrap position of the last chosen input)
+// + 1 draws -- read off the stored potential mask.
+__device__ __forceinline__ uint32_t sp_sample_draws(const SpInitCfg& c, const uint32_t* prow, int col) {
+    const int nin = c.nin;
+    const int32_t c0 = sp_column_center(c, col) % nin;
+    for (int d = nin - 1; d >= 0; d--) {
+        int in = c0 + d;
+        if (in >= nin) in -= nin;
+        if ((prow[in >> 5] >> (in & 31)) & 1u) return (uint32_t)d + 1u;
+    }
+    return 0u;
+}
+
+// Paged engines: sp_init_kernel's draws for columns col_from..col_hi of
+// stream s (one 8-column checkpoint group), replayed by ONE lane from the
+// group's checkpoint: write(col, rank, p) receives every initial permanence in
+// potential order.  Draws of the group's earlier columns and every column's
+// sampling draws are skipped (whole 31-draw blocks advance the state without
+// output); then every 4 draws give one permanence.  Registers only.
+template <class W>
+__device__ __forceinline__ void sp_replay_init(const SpInitCfg& c, int s, int col_from, int col_hi, W&& write) {
+    const int pw = c.nin_pad >> 5;
+    const int g0 = col_from - col_from % SP_CKPT_COLS;
+    const uint32_t* pot = c.potmask + (size_t)s * c.ncol * pw;
+    const uint32_t npd = 4u * (uint32_t)c.n_potential;  // permanence draws of a column
+    // sampling draws of the group's columns, 16 bits each (<= nin <= 32768)
+    uint64_t dlo = 0, dhi = 0;
+    for (int k = 0; k < SP_CKPT_COLS && g0 + k <= col_hi; k++) {
+        const uint64_t d = sp_sample_draws(c, pot + (size_t)(g0 + k) * pw, g0 + k);
+        if (k < 4) dlo |= d << (16 * k);
+        else dhi |= d << (16 * (k - 4));
+    }
+    auto draws = [&](int col) -> uint32_t {
+        const int k = col - g0;
+        return (uint32_t)((k < 4 ? dlo >> (16 * k) : dhi >> (16 * (k - 4))) & 0xFFFFull);
+    };
+    uint64_t sk = 0;  // draws to discard before the next permanence draw
+    for (int k = g0; k < col_from; k++) sk += draws(k) + npd;
+    sk += draws(col_from);
+    int col = col_from;
+    uint32_t i = 0, q0 = 0, q1 = 0, q2 = 0;
+    auto take = [&](uint32_t raw) {
+        if (col > col_hi) return;
+        if (sk) {
+            sk--;
+            return;
+        }
+        const uint32_t ph = i & 3u;
+        if (ph == 0) q0 = raw;
+        else if (ph == 1) q1 = raw;
+        else if (ph == 2) q2 = raw;
+        else {
+            bool isconn;
+            write(col, (int)(i >> 2), sp_init_value(c, q0, q1, q2, raw, isconn));
+        }
+        if (++i == npd) {
+            i = 0;
+            col++;
+            if (col <= col_hi) sk = draws(col);
+        }
+    };
+    const uint32_t* ck = c.ckpt + ((size_t)s * c.n_ckpt + (size_t)(g0 / SP_CKPT_COLS)) * SP_CKPT_WORDS;
+    uint32_t st[31];
+#pragma unroll
+    for (int j = 0; j < 31; j++) st[j] = ck[j];
+    // draws the checkpoint's block had generated but not handed out yet
+    for (uint32_t j = ck[31]; j < 31u; j++) take(ck[32 + j]);
+    while (col <= col_hi) {
+        if (sk >= 31) {
+#pragma unroll
+            for (int j = 0; j < 31; j++) st[(3 + j) % 31] += st[j];
+            sk -= 31;
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < 31; j++) {
+            const int f = (3 + j) % 31;
+            st[f] += st[j];
+            take((st[f] >> 1) & 0x7fffffffu);
+        }
+    }
+}
+
+// The initial permanences of one column into a fresh pool row: out of line,
+// so the rare replay does not weigh on the fused kernels' register budget
+static __device__ __attribute__((noinline)) void sp_regen_row(SpInitCfg c, int s, int col, float* row) {
+    sp_replay_init(c, s, col, col, [&](int, int k, float p) { row[k] = p; });
+}
+
+// Permanence row of column col of stream s (wave-uniform; every lane of the
+// wave calls it).  Paged engines hand a column a pool row on its first change
+// (lane 0 regenerates the initial values into it); null when the pool is
+// exhausted (flagged SP_ERR_POOL: the update is dropped, results invalid).
+template <bool PAGED_OK>
+__device__ __forceinline__ float* sp_perm_row(const DevCfg& c, const SpBufs& b, int s, int col) {
+    const size_t ms = (size_t)model_stream(c, s);
+    if (!PAGED_OK || !c.sp_paged) return b.perm + (ms * c.ncol + col) * c.n_potential;
+    uint32_t r = 0, fresh = 0;
+    if (lane_id() == 0) {
+        uint32_t* slot = b.prow + ms * c.ncol + col;
+        r = *slot;
+        if (r == SP_ROW_NONE) {
+            const unsigned long long x = atomicAdd(b.pool_next, 1ull);
+            if (x < c.pool_rows) {
+                r = (uint32_t)x;
+                sp_regen_row(sp_init_cfg(c, b), (int)ms, col, b.pool + (size_t)r * c.pool_stride);
+                *slot = r;
+                fresh = 1;
+            } else {
+                atomicOr(&b.err[s], SP_ERR_POOL);
+            }
+        }
+    }
+    r = (uint32_t)__shfl((int)r, 0, 64);
+    // lane 0's stores of a fresh row before the wave's loads of it (rows are
+    // 128-byte aligned and handed out once, so no cache line holds an older copy)
+    if (__shfl((int)fresh, 0, 64)) __threadfence();
+    if (r == SP_ROW_NONE) return nullptr;
+    return b.pool + (size_t)r * c.pool_stride;
+}
+
 // updatePermanencesForColumn_ on one potential permanence: returns the new
 // value and whether it is connected (>= synPermConnected - epsilon, tested
 // after the raise-clip and before the trim-clip).
@@ -182,12 +367,14 @@ __device__ __forceinline__ float sp_update_perm(const DevCfg& c, float p, bool r
 // One wave adapts one column: lane l owns inputs [8l, 8l+8) of each 512-bit
 // chunk of the potential mask.  mode 0: adaptSynapses_ (+inc/-dec by input),
 // mode 1: bumpUpWeakColumns_ (+synPermBelowStimulusInc, no raise).
+template <bool PAGED_OK>
 __device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b, int s, int col, const uint32_t* in_bits, int mode) {
     const int l = lane_id();
     const int pw = c.nin_pad >> 5;
     const size_t ms = (size_t)model_stream(c, s);
     const uint32_t* prow = b.potmask + (ms * c.ncol + col) * pw;
-    float* perm = b.perm + (ms * c.ncol + col) * c.n_potential;
+    float* perm = sp_perm_row<PAGED_OK>(c, b, s, col);
+    if (!perm) return;
     uint32_t* connT = b.connT + ms * c.nin_pad * c.nw;
     const uint32_t cw = (uint32_t)col >> 5, cb = 1u << (col & 31);
     int rank_base = 0;
@@ -270,7 +457,9 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
 // One SpatialPooler.compute of stream s by the calling workgroup (>= 64
 // threads; learning uses every wave).  sh may live in static or dynamic LDS;
 // `input` is the encoder values (SpShared) or the input SDR (SpSharedSdr).
-template <bool LEARN, class SH, class IN>
+// PAGED_OK = false compiles the paged-permanence path out (kernels that
+// never run paged engines: the frozen-inference bench kernel).
+template <bool LEARN, bool PAGED_OK = true, class SH, class IN>
 __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, const IN* input, int s,
                                              SH& sh, int write_overlaps) {
     const int t = threadIdx.x;
@@ -283,7 +472,7 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     if (t == 0) b.nact[s] = (uint32_t)nact;
     if (!LEARN) return;  // (callers synchronise before reading b.act)
     // ---- adaptSynapses_: one wave per active column
-    for (int a = wave_id(); a < nact; a += blockDim.x >> 6) sp_adapt_column(c, b, s, sh.actlist[a], sh.in, 0);
+    for (int a = wave_id(); a < nact; a += blockDim.x >> 6) sp_adapt_column<PAGED_OK>(c, b, s, sh.actlist[a], sh.in, 0);
     __syncthreads();
     // ---- updateDutyCycles_ (period = min(dutyCyclePeriod, iterationNum))
     float* odc = b.duty + (size_t)model_stream(c, s) * 2 * c.ncol;
@@ -312,7 +501,7 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     const int nb = sh.nbump;
     if (nb > 0) {
         // ascending order is irrelevant: each column is updated independently
-        for (int k = wave_id(); k < nb; k += blockDim.x >> 6) sp_adapt_column(c, b, s, sh.bump[k], sh.in, 1);
+        for (int k = wave_id(); k < nb; k += blockDim.x >> 6) sp_adapt_column<PAGED_OK>(c, b, s, sh.bump[k], sh.in, 1);
     }
     // ---- isUpdateRound_: updateMinDutyCyclesGlobal_
     if (sh.iter % (uint32_t)c.update_period == 0) {

@@ -2583,7 +2583,7 @@ __device__ __forceinline__ void bt_helper(const DevCfg& c, const TmBufs& b, uint
     }
 }
 
-template <bool LEARN, bool FROZEN>
+template <bool LEARN, bool FROZEN, bool PAGED_OK>
 __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
                                              float* scores, int n_steps, int sp_learn, int keep_prev,
                                              int keep_overlaps, uint32_t* wq, int unit_steps, int n, BtArgs bt) {
@@ -2641,8 +2641,8 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
             k = k0;
         }
         const double* v = values + (size_t)k * c.n_streams * c.n_fields;
-        if (sp_learn) sp_step_body<true>(c, sp, v, s, ssh, keep_overlaps);
-        else sp_step_body<false>(c, sp, v, s, ssh, keep_overlaps);
+        if (sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps);
+        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps);
         __syncthreads();
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
                                     k == k1 - 1, bt_ep);
@@ -2676,11 +2676,15 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 
 __global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_kernel(
     HTM_RUN_ARGS) {
-    htm_run_body<false, true>(HTM_RUN_PASS);
+    htm_run_body<false, true, false>(HTM_RUN_PASS);
+}
+// the same for engines with paged SP permanences (SP learning may page in rows)
+__global__ __launch_bounds__(TM_NT) void htm_run_frozen_paged_kernel(HTM_RUN_ARGS) {
+    htm_run_body<false, true, true>(HTM_RUN_PASS);
 }
 template <bool LEARN>
 __global__ __launch_bounds__(TM_NT) void htm_run_kernel(HTM_RUN_ARGS) {
-    htm_run_body<LEARN, false>(HTM_RUN_PASS);
+    htm_run_body<LEARN, false, true>(HTM_RUN_PASS);
 }
 
 static int run_grid(const void* fn, size_t lds, int total) {
@@ -2716,11 +2720,13 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     // a single unit per stream runs on the hardware dispatcher (grid = streams)
     if (nblk > 1 && hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
     const void* fn = tm_learn ? (const void*)htm_run_kernel<true>
-                     : frozen ? (const void*)htm_run_frozen_kernel
+                     : frozen ? (c.sp_paged ? (const void*)htm_run_frozen_paged_kernel : (const void*)htm_run_frozen_kernel)
                               : (const void*)htm_run_kernel<false>;
     const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
     if (tm_learn)
         hipLaunchKernelGGL((htm_run_kernel<true>), dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
+    else if (frozen && c.sp_paged)
+        hipLaunchKernelGGL(htm_run_frozen_paged_kernel, dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
     else if (frozen)
         hipLaunchKernelGGL(htm_run_frozen_kernel, dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
     else
@@ -3018,9 +3024,11 @@ int tm_configure_lds(const DevCfg& c) {
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
     hipError_t e5 = hipFuncSetAttribute((const void*)htm_run_kernel<false>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
+    hipError_t e6 = hipFuncSetAttribute((const void*)htm_run_frozen_paged_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
     (void)hipGetLastError();
     return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess && e4 == hipSuccess &&
-            e5 == hipSuccess)
+            e5 == hipSuccess && e6 == hipSuccess)
                ? 0
                : -1;
 }

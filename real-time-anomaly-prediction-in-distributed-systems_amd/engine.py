@@ -211,6 +211,8 @@ class HTMEngine:
     def import_state(self, region: str, data: np.ndarray, s0: int = 0):
         data = np.ascontiguousarray(data)
         per = self.state_bytes(region)
+        if region == "sp_perm_ckpt" and (per == 0 or data.nbytes == 0):
+            return  # SP checkpoints exist only in paged engines: none given or none held, keep the stream's own
         n = data.nbytes // per
         check(self._L.htm_import_state(self.h, ST[region], s0, n, data.ctypes.data_as(ctypes.c_void_p), data.nbytes))
 
@@ -224,6 +226,10 @@ class HTMEngine:
 
     def device_bytes(self) -> int:
         return self._L.htm_device_bytes(self.h)
+
+    def sp_perm_rows_used(self) -> int:
+        """Paged SP permanences: pool rows handed out (0 for a dense engine)."""
+        return int(self._L.htm_sp_perm_rows_used(self.h))
 
     def profile(self, on: bool):
         """Bracket every step's SP and TM kernels with HIP events."""

@@ -35,15 +35,16 @@ def test_struct_layouts_match_the_header(rt, tmp_path):
     src = tmp_path / "probe.c"
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n'
-        'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(htm_config), sizeof(htm_tm_header),'
+        'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(htm_config), sizeof(htm_tm_header),'
         ' sizeof(htm_tm_update), offsetof(htm_config, tm_seed), offsetof(htm_tm_header, inf_pat_head),'
-        ' offsetof(htm_config, sdr_bits));}\n' % HEADER)
+        ' offsetof(htm_config, sdr_bits), offsetof(htm_config, sp_perm_rows));}\n' % HEADER)
     exe = tmp_path / "probe"
     assert os.system(f"gcc {src} -o {exe}") == 0
     vals = [int(x) for x in os.popen(str(exe)).read().split()]
     L = rt._lib
     assert vals == [ctypes.sizeof(L.HtmConfig), ctypes.sizeof(L.TmHeader), ctypes.sizeof(L.TmUpdate),
-                    L.HtmConfig.tm_seed.offset, L.TmHeader.inf_pat_head.offset, L.HtmConfig.sdr_bits.offset]
+                    L.HtmConfig.tm_seed.offset, L.TmHeader.inf_pat_head.offset, L.HtmConfig.sdr_bits.offset,
+                    L.HtmConfig.sp_perm_rows.offset]
 
 
 def test_default_config_is_the_reference_model1(rt):
@@ -61,7 +62,7 @@ def test_default_config_is_the_reference_model1(rt):
 
 def test_abi_version_and_error_string(rt):
     L = rt._lib.lib()
-    assert L.htm_abi_version() == 2
+    assert L.htm_abi_version() == 3
     assert isinstance(L.htm_last_error(), bytes)
 
 

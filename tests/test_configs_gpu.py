@@ -3,9 +3,11 @@ independent oracle models on sampled streams, plus the size-independent
 properties the domain offers (identical inputs -> identical outputs; a stream
 is unaffected by the other streams of its launch).
 
-Config 3: 65,536 streams learning on (BASELINE configs[2]) -- here 512 fresh
+Config 3: 65,536 streams learning on (BASELINE configs[2]) with the paged SP
+          permanences the bench uses (htm_config.sp_perm_rows): 512 fresh
           streams with per-stream seeds, every step of 8 sampled streams
-          checked against the oracle and the full SP/TM state of two.
+          checked against the oracle and the full SP/TM state of two; and the
+          full 65,536 streams, 5 sampled streams against the oracle.
 Config 4: fleet mode, 131,072 streams sharing one frozen model (configs[3]).
 Config 5: the cpu / mem / mean / max response-time aggregate
           (StreamEngine/StreamAggregator.py:101-115) through a 4-field
@@ -82,7 +84,7 @@ def test_config3_many_fresh_streams_learning(rt, oracle_mod):
     streams match independent oracle models at every step; two of them match
     in their whole SP/TM state at the end."""
     n, T = 512, 120
-    eng = rt.HTMEngine(n, seed_stride=1, seg_capacity=1 << 13)
+    eng = rt.HTMEngine(n, seed_stride=1, seg_capacity=1 << 13, sp_perm_rows=1536)
     rng = np.random.default_rng(41)
     base = rng.integers(0, 101, size=(40, 1)).astype(np.float64)
     vals = np.clip(np.tile(base, (3, n)) + rng.integers(-4, 5, size=(T, n)), 0, 100)
@@ -99,6 +101,29 @@ def test_config3_many_fresh_streams_learning(rt, oracle_mod):
     for s in (sample[2], sample[-1]):
         sp_equal(eng, s, orcs[s])
         tm_equal(eng, s, orcs[s])
+
+
+def test_config3_65536_streams_paged_vs_oracle(rt, oracle_mod, traces):
+    """Config 3 at its stated size: 65,536 fresh learning streams (seed 2045 + s)
+    on one GPU with paged SP permanences, the bench's inputs (trace + jitter),
+    32 lockstep steps; 5 sampled streams equal independent oracle models at
+    every step, one of them in its whole SP state."""
+    import bench
+    n, T = 65536, 32
+    trace = np.asarray(traces["test"], np.float64)
+    vals = bench.make_inputs(n, 0, n, 0, T, trace)
+    cfg = rt.default_config(seg_capacity=10240, upd_capacity=512, seed_stride=1, sp_perm_rows=800)
+    eng = rt.HTMEngine(n, config=cfg)
+    v = torch.tensor(vals, device="cuda")
+    got = np.stack([eng.step(v[k]).cpu().numpy() for k in range(T)])
+    eng.status()
+    assert 0 < eng.sp_perm_rows_used() <= n * 800
+    for s in (0, 1, 31337, 40961, n - 1):
+        o = oracle_mod.OracleModel(sp_seed=2045 + s, tm_seed=2045 + s)
+        want = np.array([o.step([vals[k, s]], True, True) for k in range(T)], np.float32)
+        assert np.array_equal(got[:, s], want), f"stream {s}"
+        if s == n - 1:
+            sp_equal(eng, s, o)
 
 
 # response times in ms next to cpu/mem percent: per-field encoder ranges
