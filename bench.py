@@ -564,6 +564,10 @@ def timed_replay(eng, vals, scores, a, steps, mode, chunk, gather, gathered, ran
             if gather is not None:
                 h, _ = gather.gather(scores[a + k], staging=gathered[k] if rank == 0 else None)
                 handles.append(h)
+        # the deferred dutyCycle() writes of these steps are part of the work
+        # (HTM_OPT_DEFER_DUTY): completed inside the timed region
+        if hasattr(eng, "flush"):
+            eng.flush()
     for h in handles:
         h.wait()
     sync()

@@ -156,7 +156,18 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    the serial loop in every mode (measured: no faster) */
 #define HTM_OPT_BT_TAIL 9       /* helpers join a launch's backtracks once at most this many owners are
                                    still running (default 64) */
+#define HTM_OPT_DEFER_DUTY 10   /* 1 (default): in frozen lockstep steps (htm_step), a phase 2 whose
+                                   confidences the step discards (backtrack replays, out-of-sequence
+                                   results) computes only the predicted cells; the first dutyCycle()
+                                   record write of its qualifying segments is deferred to a flush kernel
+                                   (every 16 steps, and before any call that reads the records: export,
+                                   save, learning on, htm_status / htm_counters, htm_flush).  Results and
+                                   state are those of the undeferred step.  0: count every phase 2 in full */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
+
+/* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY) on `stream`
+ * (asynchronous): a benchmark's timed region ends with it. */
+int htm_flush(htm_engine* eng, void* stream);
 
 /* Kernel times of the profiled launches since the last call (synchronises):
  * out4 = {SP kernel ms, TM (or fused SP+TM) kernel ms, steps covered,

@@ -45,6 +45,7 @@ OPT_RUN_CHUNK = 6
 OPT_RUN_UNIT = 7
 OPT_BT_ASSIST = 8
 OPT_BT_TAIL = 9
+OPT_DEFER_DUTY = 10
 
 
 class HtmConfig(ctypes.Structure):
@@ -109,7 +110,7 @@ EXPORTED = [
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_sp_perm_rows_used", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
     "htm_profile_read", "htm_counters", "htm_debug_stamps",
-    "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats", "htm_create_fleet", "htm_is_fleet",
+    "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats", "htm_create_fleet", "htm_is_fleet", "htm_flush",
     "htm_likelihood_create", "htm_likelihood_destroy", "htm_likelihood_step",
     "htm_cls_create", "htm_cls_destroy", "htm_cls_compute", "htm_cls_status", "htm_cls_state_bytes",
     "htm_cls_export_state", "htm_cls_import_state",
@@ -183,6 +184,7 @@ def lib():
     L.htm_counters.argtypes = [vp, P(ctypes.c_uint64)]
     L.htm_debug_stamps.argtypes = [vp, P(ctypes.c_uint64)]
     L.htm_create_fleet.argtypes = [vp, i32, i32, i32, i32, P(vp)]
+    L.htm_flush.argtypes = [vp, vp]
     L.htm_is_fleet.argtypes = [vp]
     L.htm_is_fleet.restype = i32
     L.htm_likelihood_create.argtypes = [i32, i32, i32, i32, i32, i32, P(vp)]

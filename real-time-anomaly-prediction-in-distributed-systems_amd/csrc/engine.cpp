@@ -83,7 +83,12 @@ struct htm_engine {
     int32_t bt_tail = 64;           // HTM_OPT_BT_TAIL: owners left when helpers join
     uint32_t bt_epoch = 0;          // last assisted launch's tag
     unsigned long long bt_base = 0; // workgroups counted by bt_ctl before the next assisted launch
+    int32_t defer = 1;              // HTM_OPT_DEFER_DUTY: frozen lockstep steps defer discarded phase 2s' duty writes
+    int32_t defer_steps = 0;        // lockstep launches since the last flush of the deferred log
+    int32_t flush_every = 0;        // lockstep launches between flushes (0: fx_dcap / 2)
 };
+
+static int flush_deferred(htm_engine* e, hipStream_t st);
 
 extern "C" {
 
@@ -273,6 +278,10 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     if (const char* env = std::getenv("HTM_FX_PID"))  // A/B knob: 0 = no pid lists (rows path)
         if (std::atoi(env) == 0) d.fx_pcap = 0;
     d.fx_noff = d.ncells * d.fx_nwin + d.ncells + 1;
+    // deferred phase-2 log entries per stream (lockstep): a flush every
+    // fx_dcap / 2 steps keeps them from filling (a full log falls back to
+    // counting in the step)
+    d.fx_dcap = n <= 16384 ? 32 : 8;
     return HTM_OK;
 }
 
@@ -432,6 +441,8 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     }
     if (const char* env = std::getenv("HTM_FUSED")) e->fused = std::atoi(env) != 0;  // A/B knob
     if (const char* env = std::getenv("HTM_RUN_UNIT")) e->run_unit = std::max(1, std::atoi(env));  // A/B knob
+    if (const char* env = std::getenv("HTM_DEFER_DUTY")) e->defer = std::atoi(env) != 0;            // A/B knob
+    if (const char* env = std::getenv("HTM_DEFER_FLUSH_EVERY")) e->flush_every = std::max(1, std::atoi(env));  // test knob
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
         // shapes whose fixed LDS state leaves no room at 3 workgroups per CU
@@ -508,6 +519,7 @@ int htm_destroy(htm_engine* e) {
 
 int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (int r = flush_deferred(e, nullptr)) return r;
     if (e->fleet && (sp_learn || tm_learn))
         return htm_fail(HTM_E_STATE, "a fleet engine shares one frozen model: learning stays off");
     e->sp_learn = sp_learn ? 1 : 0;
@@ -540,6 +552,12 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         if (value < 1) return htm_fail(HTM_E_INVALID, "run chunk must be >= 1");
         e->run_chunk = value;
     }
+    else if (opt == HTM_OPT_DEFER_DUTY) {
+        if (!value) {
+            if (int r = flush_deferred(e, nullptr)) return r;
+        }
+        e->defer = value ? 1 : 0;
+    }
     else if (opt == HTM_OPT_BT_ASSIST) e->bt_assist = value < 0 ? 0 : value > 2 ? 2 : value;
     else if (opt == HTM_OPT_BT_TAIL) e->bt_tail = value < 0 ? 0 : value > 0xFFFFFF ? 0xFFFFFF : value;
     else if (opt == HTM_OPT_RUN_UNIT) {
@@ -565,12 +583,33 @@ static int alloc_fx(htm_engine* e) {
     ALLOC(e->tm.fx_nr, uint32_t, M);
     ALLOC(e->tm.fx_pcell, uint16_t, M * (size_t)d.fx_pcap);
     ALLOC(e->tm.fx_np, uint32_t, M);
+    // deferred dutyCycle() writes of lockstep steps: a log per stream, the
+    // flush kernel's per-workgroup qualifying lists
+    const size_t S = (size_t)e->n;
+    ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * (size_t)d.max_act_cells);
+    ALLOC(e->tm.fx_dlen, uint16_t, S * (size_t)d.fx_dcap);
+    ALLOC(e->tm.fx_dn, uint32_t, S);
+    ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
+    ALLOC(e->tm.fx_fwork, uint32_t, 1);
+    return HTM_OK;
+}
+
+// Replay the deferred dutyCycle() writes logged by lockstep steps (asynchronous
+// on `st`).  Called before anything reads or rebuilds the segment records.
+static int flush_deferred(htm_engine* e, hipStream_t st) {
+    if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
+    HIP_TRY(hipMemsetAsync(e->tm.fx_fwork, 0, 4, st));
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, st))
+        return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipMemsetAsync(e->tm.fx_dn, 0, (size_t)e->n * 4, st));
+    e->defer_steps = 0;
     return HTM_OK;
 }
 
 static int build_fx(htm_engine* e, hipStream_t st) {
     const DevCfg& d = e->dc;
-    int ra = alloc_fx(e);
+    int ra = flush_deferred(e, st);  // the log refers to the index being replaced
+    if (!ra) ra = alloc_fx(e);
     if (ra) return ra;
     if (launch_tm_fx_rank(d, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "fx rank launch");
     if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return htm_fail(HTM_E_HIP, "fx count launch");
@@ -618,6 +657,11 @@ static int next_events(htm_engine* e, hipEvent_t* ev, int32_t steps) {
 // with TM learning off the frozen forward index is (re)built first.
 static int prepare_step(htm_engine* e, hipStream_t st, int* frozen) {
     *frozen = 0;
+    if (e->tm_learn || !e->use_frozen) {
+        // the pool scans read the segments' dutyCycle records
+        int r = flush_deferred(e, st);
+        if (r) return r;
+    }
     if (e->tm_learn) {
         e->fx_valid = false;
     } else if (e->use_frozen) {
@@ -658,9 +702,16 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     } else {
         tb.bt_state = nullptr;  // the kernel's "off" test
     }
+    // deferred dutyCycle() writes: frozen lockstep launches (one step), not assisted
+    const bool defer = frozen && n_steps == 1 && e->defer && tb.fx_dlog && !tb.bt_state;
+    if (!defer) tb.fx_dlog = nullptr;
     if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, bt, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
+    if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : e->dc.fx_dcap / 2)) {
+        int r = flush_deferred(e, st);
+        if (r) return r;
+    }
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
 }
@@ -683,7 +734,9 @@ static int step_unfused(htm_engine* e, const double* d_values, const uint32_t* d
         if (launch_prev_pred(e->dc, e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "prev_pred launch");
     }
     if (e->profile) HIP_TRY(hipEventRecord(ev[1], st));
-    if (launch_tm_step(e->dc, e->tm, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
+    TmBufs tb = e->tm;
+    tb.fx_dlog = nullptr;  // (deferred duty writes: fused lockstep launches only)
+    if (launch_tm_step(e->dc, tb, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
         return htm_fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
@@ -750,6 +803,7 @@ int htm_profile_read(htm_engine* e, double* out4) {
 // pool high-water marks, OR of error flags}
 int htm_counters(htm_engine* e, uint64_t* out8) {
     if (!e || !out8) return htm_fail(HTM_E_INVALID, "bad arguments");
+    if (int r = flush_deferred(e, nullptr)) return r;
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
@@ -995,6 +1049,7 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
         return htm_fail(HTM_E_INVALID, "bad export arguments");
     const Region& r = e->regions[region];
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "export buffer too small");
+    if (int rf = flush_deferred(e, nullptr)) return rf;
     HIP_TRY(hipDeviceSynchronize());
     if (r.per_stream == 0) return HTM_OK;
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_export(e, s0, n, h_dst, nullptr);
@@ -1022,6 +1077,7 @@ static int import_region(htm_engine* e, int32_t region, int32_t s0, int32_t n, c
     // no checkpoints (an export of a dense engine): the streams keep their own
     if (region == HTM_ST_SP_PERM_CKPT && (bytes == 0 || r.per_stream == 0)) return HTM_OK;
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "import buffer too small");
+    if (int rf = flush_deferred(e, nullptr)) return rf;
     HIP_TRY(hipDeviceSynchronize());
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_import(e, s0, n, h_src, nullptr, 0);
     if (rebase && e->dc.sp_paged && (region == HTM_ST_SP_PERM_CKPT || region == HTM_ST_SP_POTMASK))
@@ -1071,6 +1127,7 @@ static int replicate_region(uint8_t* base, size_t per, int32_t src, int32_t n, h
 int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     if (!e || src < 0 || src >= e->n) return htm_fail(HTM_E_INVALID, "bad source stream");
     hipStream_t st = (hipStream_t)stream;
+    if (int rf = flush_deferred(e, st)) return rf;
     for (int id = 1; id <= HTM_ST_COUNT; id++) {
         const Region& r = e->regions[id];
         if (!r.base || !r.per_stream) continue;
@@ -1107,6 +1164,7 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
     if (model_stream < 0 || model_stream >= model->n) return htm_fail(HTM_E_INVALID, "bad model stream");
     *out = nullptr;
     HIP_TRY(hipSetDevice(model->device));
+    if (int rf = flush_deferred(const_cast<htm_engine*>(model), nullptr)) return rf;
     HIP_TRY(hipDeviceSynchronize());
     htm_engine* e = nullptr;
     htm_config fcfg = model->cfg;
@@ -1148,6 +1206,11 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
 
 int32_t htm_is_fleet(const htm_engine* e) { return e && e->fleet ? 1 : 0; }
 
+int htm_flush(htm_engine* e, void* stream) {
+    if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    return flush_deferred(e, (hipStream_t)stream);
+}
+
 int32_t htm_n_streams(const htm_engine* e) { return e ? e->n : 0; }
 
 int htm_get_config(const htm_engine* e, htm_config* out) {
@@ -1176,6 +1239,7 @@ int32_t htm_abi_version(void) { return HTM_ABI_VERSION; }
 // Synchronise and report per-stream error flags (pool/queue overflow).
 int htm_status(htm_engine* e) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (int r = flush_deferred(e, nullptr)) return r;
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));

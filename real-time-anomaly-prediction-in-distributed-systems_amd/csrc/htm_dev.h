@@ -63,6 +63,7 @@ struct DevCfg {
     int32_t shared_model;                 // fleet: every stream reads model instance 0 (SP + TM frozen)
     int32_t q_cap;                        // per-stream capacity of the qualifying-segment scratch lists
     int32_t sdr_in;                       // the SP reads an external input SDR of nin bits (no encoder)
+    int32_t fx_dcap;                      // deferred phase-2 log entries per stream (TmBufs::fx_dlog)
     // paged SP permanences (htm_config.sp_perm_rows > 0)
     int32_t sp_paged;                     // 1: rows from SpBufs::pool on first change, else init values
     int32_t n_ckpt;                       // nupic::Random checkpoints per stream (ncol / SP_CKPT_COLS)
@@ -156,7 +157,20 @@ struct TmBufs {
     uint16_t* bt_pat;              // [S][HTM_MAXPAT][HTM_MAXACT] posted pattern history (oldest first)
     uint32_t* bt_info;             // [S][BT_INFO_WORDS] numPrev, lrn_iter, avg density (2 words), lengths
     unsigned long long* bt_ctl;    // [3] workgroups started, owners done, helper slots taken (monotonic)
+    // Deferred dutyCycle() writes (frozen lockstep launches; null: off).  A
+    // frozen phase 2 whose confidences the step discards needs only the
+    // predicted cells (the pid pass) for what follows; its one remaining effect,
+    // the first dutyCycle() record write of each qualifying segment (FX_FRESH),
+    // is deferred: the phase 2's active cells are logged, and
+    // tm_fx_flush_kernel replays the log before anything reads the records.
+    uint16_t* fx_dlog;             // [S][fx_dcap][max_act_cells] active cells of a deferred phase 2
+    uint16_t* fx_dlen;             // [S][fx_dcap] their number
+    uint32_t* fx_dn;               // [S] entries logged since the last flush
+    uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
+    uint32_t* fx_fwork;            // [1] flush work counter
 };
+
+#define FX_FLUSH_WG 1024  // persistent workgroups of tm_fx_flush_kernel (each has its own scratch list)
 
 #define BT_INFO_WORDS (4 + HTM_MAXPAT)
 #define FX_FRESH 0x80000000u  // fx_rec.x: the segment's dutyCycle record holds its frozen value
@@ -363,6 +377,7 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
                    uint32_t* wq, int unit_steps, BtArgs bt, hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen);

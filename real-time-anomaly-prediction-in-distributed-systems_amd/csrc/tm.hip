@@ -52,6 +52,8 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t ncand;
     int32_t ti[8];
     int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
+    int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
+    int32_t fx_slot;    // deferred-log slot of this phase 2, or -1
     float tf[4];
     uint32_t red[3 * TM_NWAVES];
     uint16_t act[HTM_MAXACT];
@@ -94,6 +96,7 @@ struct Tm {
     uint32_t nr;       // ranks (live segments) of the frozen index
     const TmBufs* tb;  // the engine's buffers (backtrack assist)
     uint32_t bt_epoch; // > 0: this launch's backtracks are assisted (frozen lockstep)
+    bool defer;        // discarded frozen phase 2s log their active cells (TmBufs::fx_dlog)
 };
 
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
@@ -523,7 +526,12 @@ __device__ __forceinline__ void wg_clear4(uint32_t* p, uint32_t nquads) {
 // activationThreshold predicts the segment's cell); then, per window of the
 // slot space, all active synapses of every segment (counter >= thr: the
 // segment qualifies for the confidence sum).
-__device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
+// what collect_frozen counts: the pid pass and every rank window, the pid pass
+// only, or the rank windows only (listing the active cells, or reusing the
+// list a pid-only call left in U)
+enum { FX_ALL = 0, FX_PID = 1, FX_WIN = 2, FX_WIN_REUSE = 3 };
+
+__device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const uint32_t W = (uint32_t)c.fx_win;
@@ -534,8 +542,14 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
     uint32_t* pstart = t.U + W / 4 + 64 + (mac + 1) / 2;
     uint32_t* plo = pstart + mac + 1;
     uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
-    const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
-    const uint32_t na = nact < mac ? nact : mac;
+    uint32_t na;
+    if (mode == FX_WIN_REUSE) {
+        na = (uint32_t)sh->fx_na;
+    } else {
+        const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
+        na = nact < mac ? nact : mac;
+        if (threadIdx.x == 0) sh->fx_na = (int32_t)na;
+    }
     const uint32_t nr = t.nr;
     STAMP(t, SB_LIST);
     COUNT(t, SC_NACT, na);
@@ -564,9 +578,10 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
             }
         }
     };
-    const int w_first = (pid_ok && t.np > 0) ? -1 : 0;
-    load_offsets(w_first);
-    for (int w = w_first; w < (int)nw; w++) {
+    const int w_first = (pid_ok && t.np > 0 && mode != FX_WIN && mode != FX_WIN_REUSE) ? -1 : 0;
+    const int w_end = mode == FX_PID ? 0 : (int)nw;
+    if (w_first < w_end) load_offsets(w_first);
+    for (int w = w_first; w < w_end; w++) {
         // list of (active cell k, pass w): block range [fxoff[idx], fxoff[idx + 1])
         uint32_t lsum = 0;
 #pragma unroll
@@ -587,7 +602,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
             pstart[k] = hi - lo;
             lsum += hi - lo;
         }
-        if (w + 1 < (int)nw) load_offsets(w + 1);
+        if (w + 1 < w_end) load_offsets(w + 1);
         uint32_t B;
         uint32_t pos = wg_excl_scan1(sh, lsum, &B);
         for (uint32_t j = 0; j < per; j++) {
@@ -626,7 +641,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr) {
         STAMP(t, SB_QSCAN);
     }
     // out-list blocks + the two block offsets of every (active cell, pass)
-    if (threadIdx.x == 0) sh->bytes += 16ull * nblk + 8ull * na * (nw + (pid_ok && t.np > 0 ? 1u : 0u));
+    if (threadIdx.x == 0 && w_end > w_first) sh->bytes += 16ull * nblk + 8ull * na * (uint32_t)(w_end - w_first);
 }
 
 // Pass 1 of _inferPhase2 over the qn qualifying segments in t.q1: the
@@ -1080,6 +1095,37 @@ __device__ __forceinline__ void phase2_duty_only(Tm& t) {
     COUNT(t, SC_P2, 1);
 }
 
+// Log the active cells of a frozen phase 2 whose confidences are discarded
+// (the list a pid-only collection left in U) for tm_fx_flush_kernel, which
+// makes its qualifying segments' dutyCycle() record writes.  False when the
+// stream's log is full: the caller then counts the rank windows itself.
+// Contains barriers: call uniformly.
+__device__ __forceinline__ bool defer_phase2(Tm& t) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const TmBufs& b = *t.tb;
+    if (threadIdx.x == 0) {
+        const uint32_t n = b.fx_dn[t.s];
+        sh->fx_slot = n < (uint32_t)c.fx_dcap ? (int32_t)n : -1;
+    }
+    __syncthreads();
+    const int slot = sh->fx_slot;
+    if (slot < 0) return false;
+    const uint32_t na = (uint32_t)sh->fx_na;
+    const uint32_t mac = (uint32_t)c.max_act_cells;
+    const uint16_t* cells = reinterpret_cast<const uint16_t*>(t.U + c.fx_win / 4 + 64);
+    const size_t e = (size_t)t.s * c.fx_dcap + (size_t)slot;
+    uint16_t* dst = b.fx_dlog + e * mac;
+    for (uint32_t k = threadIdx.x; k < na; k += TM_NT) dst[k] = cells[k];
+    if (threadIdx.x == 0) {
+        b.fx_dlen[e] = (uint16_t)na;
+        b.fx_dn[t.s] = (uint32_t)slot + 1u;
+        sh->bytes += 2ull * na + 8ull;
+    }
+    __syncthreads();
+    return true;
+}
+
 // _inferPhase2()
 template <bool FROZEN>
 __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
@@ -1092,6 +1138,33 @@ __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
     wg_clear(t.infP, t.c.cw);
     wg_clear(reinterpret_cast<uint32_t*>(t.colconf), t.c.ncol);
     __syncthreads();
+    if (FROZEN && t.defer && need != P2_KEEP && t.np <= (uint32_t)t.c.fx_pcap) {
+        // the predicted cells first (pid pass): a phase 2 whose confidences the
+        // step discards needs nothing else now -- its segments' one-time
+        // dutyCycle() record writes are logged for tm_fx_flush_kernel
+        collect_frozen(t, t.c.act_thr, FX_PID);
+        __syncthreads();
+        const uint32_t npc = count_predicted_cols(t);
+        const bool inSeq = (double)npc >= 0.5 * sh->avg_dens;
+        const bool keep = need == P2_IF_IN_SEQ && inSeq;
+        if (!keep && defer_phase2(t)) return inSeq;
+        collect_frozen(t, t.c.act_thr, FX_WIN_REUSE);
+        __syncthreads();
+        if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)t.c.q_cap) {
+            sh->err |= 16u;
+            sh->qn = t.c.q_cap;
+        }
+        __syncthreads();
+        if (keep) {
+            if (threadIdx.x == 0) sh->npc_known = (int32_t)npc;
+            __syncthreads();
+            (void)phase2_finish<FROZEN>(t);
+        } else {
+            phase2_duty_only(t);
+        }
+        __syncthreads();
+        return inSeq;
+    }
     if (FROZEN) collect_frozen(t, t.c.act_thr);
     else collect_scan(t, t.infA, t.c.act_thr);
     __syncthreads();
@@ -2108,6 +2181,7 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     }
     t.tb = &b;
     t.bt_epoch = 0;
+    t.defer = FROZEN && b.fx_dlog != nullptr;
 }
 
 // Write the inference state back to HBM, touching only what changed:
@@ -3009,6 +3083,8 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
     }
 }
 
+__global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n);
+
 int tm_configure_lds(const DevCfg& c) {
     // the frozen variant may exceed the default 64 KiB dynamic LDS limit
     size_t b0 = tm_step_lds_bytes(c, 1, 0), b1 = tm_step_lds_bytes(c, 0, 1), b2 = tm_step_lds_bytes(c, 0, 0);
@@ -3026,11 +3102,72 @@ int tm_configure_lds(const DevCfg& c) {
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
     hipError_t e6 = hipFuncSetAttribute((const void*)htm_run_frozen_paged_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
+    hipError_t e7 = hipFuncSetAttribute((const void*)tm_fx_flush_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
     (void)hipGetLastError();
     return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess && e4 == hipSuccess &&
-            e5 == hipSuccess && e6 == hipSuccess)
+            e5 == hipSuccess && e6 == hipSuccess && e7 == hipSuccess)
                ? 0
                : -1;
+}
+
+// Deferred dutyCycle() writes of frozen lockstep launches (TmBufs::fx_dlog):
+// each logged phase 2 is replayed -- its active cells, the rank windows'
+// counting, the first record write of every qualifying segment not yet
+// written (FX_FRESH) -- by persistent workgroups claiming (stream, entry)
+// pairs, each with its own qualifying list.  Entries of one stream may run
+// concurrently: the writes store the value every replay computes.  The bytes
+// are not added to the streams' counters (the step kernel's roofline counts
+// its own work).  The host clears fx_fwork before and fx_dn after.
+__global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ uint32_t job;
+    const uint32_t total = (uint32_t)n * (uint32_t)c.fx_dcap;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) job = atomicAdd(b.fx_fwork, 1u);
+        __syncthreads();
+        const uint32_t j = __builtin_amdgcn_readfirstlane(job);
+        if (j >= total) break;
+        const int s = (int)(j / (uint32_t)c.fx_dcap);
+        const uint32_t e = j % (uint32_t)c.fx_dcap;
+        if (e >= b.fx_dn[s]) continue;
+        Tm t;
+        tm_bind<false, true>(t, c, b, s, s, lds);
+        t.q1 = b.fx_fq + (size_t)blockIdx.x * c.q_cap;
+        t.defer = false;
+        TmSh* sh = t.sh;
+        if (threadIdx.x == 0) {
+            sh->qn = 0;
+            sh->bytes = 0;
+            sh->lrn_iter = b.hdr[s].lrn_iter;  // frozen while TM learning is off
+        }
+        wg_clear(t.infA, c.cw);
+        __syncthreads();
+        const size_t ei = (size_t)s * c.fx_dcap + e;
+        const uint32_t len = b.fx_dlen[ei];
+        const uint16_t* cl = b.fx_dlog + ei * (size_t)c.max_act_cells;
+        for (uint32_t k = threadIdx.x; k < len; k += TM_NT) atomicOr(&t.infA[cl[k] >> 5], 1u << (cl[k] & 31));
+        __syncthreads();
+        collect_frozen(t, c.act_thr, FX_WIN);
+        __syncthreads();
+        if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)c.q_cap) {
+            atomicOr(&b.hdr[s].error, 16u);  // qualifying-list overflow, as in the step
+            sh->qn = c.q_cap;
+        }
+        __syncthreads();
+        phase2_duty_only(t);
+    }
+}
+
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+    if (n <= 0 || !b.fx_dlog) return 0;
+    const size_t lds = tm_step_lds_bytes(c, 0, 1);
+    const int total = n * c.fx_dcap;
+    int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
+    if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
+    hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {

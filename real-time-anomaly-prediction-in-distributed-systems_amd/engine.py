@@ -227,6 +227,14 @@ class HTMEngine:
     def device_bytes(self) -> int:
         return self._L.htm_device_bytes(self.h)
 
+    def flush(self):
+        """Complete the deferred dutyCycle() writes of lockstep steps
+        (HTM_OPT_DEFER_DUTY) on the current stream (asynchronous)."""
+        check(self._L.htm_flush(self.h, self._stream()))
+
+    def defer_duty(self, on: bool):
+        check(self._L.htm_set_option(self.h, _lib.OPT_DEFER_DUTY, int(on)))
+
     def sp_perm_rows_used(self) -> int:
         """Paged SP permanences: pool rows handed out (0 for a dense engine)."""
         return int(self._L.htm_sp_perm_rows_used(self.h))

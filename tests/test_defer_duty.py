@@ -1,0 +1,98 @@
+"""Deferred dutyCycle() writes in frozen lockstep steps (HTM_OPT_DEFER_DUTY).
+
+A frozen phase 2 whose confidences the step discards (backtrack replays,
+out-of-sequence results) computes only the predicted cells; the first
+dutyCycle() record write of its qualifying segments is logged and replayed by
+the flush kernel.  Everything observable must equal the undeferred engine and
+the oracle: scores at every step, segment records (dutyCycle cache included)
+after any export, the phase-2 / backtrack counters -- with the log flushed on
+its cadence, and with a log that fills (the step then counts in full).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+
+@pytest.fixture(scope="module")
+def model1(rt, traces):
+    eng = rt.HTMEngine(1, seg_capacity=72 * 1024)
+    eng.run(torch.tensor(traces["train"][:2184], dtype=torch.float64, device="cuda").reshape(-1, 1))
+    eng.status()
+    return eng
+
+
+def replicas(rt, model1, n, env=None):
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        e = rt.HTMEngine(n, seg_capacity=72 * 1024)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for region in rt._lib.ST:
+        e.import_state(region, model1.export_state(region, 0, 1), s0=0)
+    e.replicate(0)
+    return e
+
+
+def lockstep(e, vals):
+    return np.stack([e.step(vals[k]).cpu().numpy() for k in range(vals.shape[0])])
+
+
+@pytest.mark.parametrize("sp_learn", [False, True])
+@pytest.mark.parametrize("env", [{}, {"HTM_DEFER_FLUSH_EVERY": "100000"}], ids=["cadence", "log_fills"])
+def test_deferred_equals_undeferred(rt, model1, traces, sp_learn, env):
+    n, T = 96, 160
+    rng = np.random.default_rng(17)
+    test = np.asarray(traces["test"], np.float64)
+    t = np.arange(T)[:, None]
+    s = np.arange(n)[None, :]
+    vals = torch.tensor(np.clip(test[(t + 53 * s) % len(test)] + rng.integers(-2, 3, size=(T, n)), 0, 100),
+                        device="cuda")
+    a = replicas(rt, model1, n, env)
+    b = replicas(rt, model1, n)
+    b.defer_duty(False)
+    for e in (a, b):
+        e.set_learning(sp_learn, False)
+    ga, gb = lockstep(a, vals), lockstep(b, vals)
+    assert np.array_equal(ga, gb)
+    ca, cb = a.counters(), b.counters()
+    for k in ("inf_phase2", "inf_backtracks", "seg_live", "error"):
+        assert ca[k] == cb[k], k
+    assert ca["inf_backtracks"] > 0
+    for region in ("tm_seg_duty", "tm_seg_meta", "tm_bitmaps", "tm_colconf", "tm_header", "sp_perm"):
+        xa, xb = a.export_state(region), b.export_state(region)
+        if region == "tm_header":  # the algorithmic byte counter differs by design
+            xa, xb = xa[:, :-8], xb[:, :-8]
+        assert np.array_equal(xa, xb), region
+
+
+def test_lockstep_test_phase_matches_golden(rt, model1, traces):
+    """ModelTesting's 1+7 steps per record (ModelTesting.py:66-72), SP learning
+    on, TM learning off, one htm_step per step with deferral on: the golden
+    windows of the oracle, and the oracle's segment records after a save."""
+    g = np.load(os.path.join(GOLDEN, "model1_golden.npz"))
+    e = replicas(rt, model1, 1)
+    e.set_learning(True, False)
+    n_rec = 300
+    v = torch.tensor(np.repeat(traces["test"][:n_rec], 8).reshape(-1, 1), device="cuda")
+    out = lockstep(e, v).reshape(n_rec, 8)
+    assert np.array_equal(out, g["test_windows"][:n_rec])
+    ref = replicas(rt, model1, 1)
+    ref.defer_duty(False)
+    ref.set_learning(True, False)
+    lockstep(ref, v)
+    sa, sb = e.tm_segments(0), ref.tm_segments(0)
+    for k in ("last_dc", "last_dc_iter", "pos_act"):
+        assert np.array_equal(sa[k], sb[k]), k
