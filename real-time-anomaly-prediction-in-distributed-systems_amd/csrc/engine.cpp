@@ -282,6 +282,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // fx_dcap / 2 steps keeps them from filling (a full log falls back to
     // counting in the step)
     d.fx_dcap = n <= 16384 ? 32 : 8;
+    if (const char* env = std::getenv("HTM_DEFER_CAP")) d.fx_dcap = std::max(1, std::atoi(env));  // A/B knob
     return HTM_OK;
 }
 
