@@ -160,7 +160,7 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    confidences the step discards (backtrack replays, out-of-sequence
                                    results) computes only the predicted cells; the first dutyCycle()
                                    record write of its qualifying segments is deferred to a flush kernel
-                                   (every 16 steps, and before any call that reads the records: export,
+                                   (every 32 steps, and before any call that reads the records: export,
                                    save, learning on, htm_status / htm_counters, htm_flush).  Results and
                                    state are those of the undeferred step.  0: count every phase 2 in full */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);

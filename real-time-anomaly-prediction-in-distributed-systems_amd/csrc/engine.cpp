@@ -280,8 +280,9 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.fx_noff = d.ncells * d.fx_nwin + d.ncells + 1;
     // deferred phase-2 log entries per stream (lockstep): a flush every
     // fx_dcap / 2 steps keeps them from filling (a full log falls back to
-    // counting in the step)
-    d.fx_dcap = n <= 16384 ? 32 : 8;
+    // counting in the step); measured on config 2 (profiles/r02_defer):
+    // 64 entries flushed every 32 steps 0.273 ms/step, 32 / 16 0.276, 16 / 8 0.304
+    d.fx_dcap = n <= 16384 ? 64 : 8;
     if (const char* env = std::getenv("HTM_DEFER_CAP")) d.fx_dcap = std::max(1, std::atoi(env));  // A/B knob
     return HTM_OK;
 }
@@ -589,7 +590,9 @@ static int alloc_fx(htm_engine* e) {
     const size_t S = (size_t)e->n;
     ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * (size_t)d.max_act_cells);
     ALLOC(e->tm.fx_dlen, uint16_t, S * (size_t)d.fx_dcap);
+    ALLOC(e->tm.fx_dhash, uint32_t, S * (size_t)d.fx_dcap);
     ALLOC(e->tm.fx_dn, uint32_t, S);
+    ALLOC(e->tm.fx_dflushed, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
     ALLOC(e->tm.fx_fwork, uint32_t, 1);
     return HTM_OK;
@@ -602,7 +605,7 @@ static int flush_deferred(htm_engine* e, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(e->tm.fx_fwork, 0, 4, st));
     if (launch_tm_fx_flush(e->dc, e->tm, e->n, st))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
-    HIP_TRY(hipMemsetAsync(e->tm.fx_dn, 0, (size_t)e->n * 4, st));
+    HIP_TRY(hipMemcpyAsync(e->tm.fx_dflushed, e->tm.fx_dn, (size_t)e->n * 4, hipMemcpyDeviceToDevice, st));
     e->defer_steps = 0;
     return HTM_OK;
 }

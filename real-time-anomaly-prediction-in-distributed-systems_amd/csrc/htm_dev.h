@@ -164,8 +164,10 @@ struct TmBufs {
     // is deferred: the phase 2's active cells are logged, and
     // tm_fx_flush_kernel replays the log before anything reads the records.
     uint16_t* fx_dlog;             // [S][fx_dcap][max_act_cells] active cells of a deferred phase 2
-    uint16_t* fx_dlen;             // [S][fx_dcap] their number
-    uint32_t* fx_dn;               // [S] entries logged since the last flush
+    uint16_t* fx_dlen;             // [S][fx_dcap] their number (a ring: entry e in slot e % fx_dcap)
+    uint32_t* fx_dhash;            // [S][fx_dcap] hash of the set
+    uint32_t* fx_dn;               // [S] entries logged (monotonic)
+    uint32_t* fx_dflushed;         // [S] entries flushed
     uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
     uint32_t* fx_fwork;            // [1] flush work counter
 };

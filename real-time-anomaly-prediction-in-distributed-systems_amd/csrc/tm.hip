@@ -53,7 +53,7 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t ti[8];
     int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
     int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
-    int32_t fx_slot;    // deferred-log slot of this phase 2, or -1
+    uint32_t fx_n, fx_f; // deferred log: entries logged, entries flushed (thread 0's copies)
     float tf[4];
     uint32_t red[3 * TM_NWAVES];
     uint16_t act[HTM_MAXACT];
@@ -1095,32 +1095,75 @@ __device__ __forceinline__ void phase2_duty_only(Tm& t) {
     COUNT(t, SC_P2, 1);
 }
 
+// murmur3's finaliser: the per-cell term of an active set's hash
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
 // Log the active cells of a frozen phase 2 whose confidences are discarded
 // (the list a pid-only collection left in U) for tm_fx_flush_kernel, which
-// makes its qualifying segments' dutyCycle() record writes.  False when the
-// stream's log is full: the caller then counts the rank windows itself.
+// makes its qualifying segments' dutyCycle() record writes.  The log is a
+// ring of fx_dcap entries per stream; an active set equal to one still in the
+// ring (flushed or not: backtrack replays recur from step to step) is not
+// logged again -- its writes are made or pending.  False when the ring holds
+// fx_dcap unflushed entries: the caller then counts the rank windows itself.
 // Contains barriers: call uniformly.
 __device__ __forceinline__ bool defer_phase2(Tm& t) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const TmBufs& b = *t.tb;
-    if (threadIdx.x == 0) {
-        const uint32_t n = b.fx_dn[t.s];
-        sh->fx_slot = n < (uint32_t)c.fx_dcap ? (int32_t)n : -1;
-    }
-    __syncthreads();
-    const int slot = sh->fx_slot;
-    if (slot < 0) return false;
+    const uint32_t dcap = (uint32_t)c.fx_dcap;
     const uint32_t na = (uint32_t)sh->fx_na;
     const uint32_t mac = (uint32_t)c.max_act_cells;
     const uint16_t* cells = reinterpret_cast<const uint16_t*>(t.U + c.fx_win / 4 + 64);
-    const size_t e = (size_t)t.s * c.fx_dcap + (size_t)slot;
-    uint16_t* dst = b.fx_dlog + e * mac;
+    const size_t s = (size_t)t.s;
+    // order-independent hash of the set
+    uint32_t h = 0;
+    for (uint32_t k = threadIdx.x; k < na; k += TM_NT) h += fmix32(cells[k] + 0x9e3779b9u);
+    if (threadIdx.x == 0) {  // (the counters are written by thread 0 only)
+        sh->fx_n = b.fx_dn[s];
+        sh->fx_f = b.fx_dflushed[s];
+    }
+    h = fmix32(wg_sum(sh, h) ^ na);
+    const uint32_t n = sh->fx_n, f = sh->fx_f;
+    // the resident entries whose hash and length match: the newest one is compared in full
+    const uint32_t resident = n < dcap ? n : dcap;
+    uint32_t cand = 0xFFFFFFFFu;
+    for (uint32_t i = threadIdx.x; i < resident; i += TM_NT) {
+        const uint32_t e = n - 1u - i;
+        const size_t slot = s * dcap + e % dcap;
+        if (b.fx_dhash[slot] == h && b.fx_dlen[slot] == na) cand = cand < i ? cand : i;
+    }
+    cand = ~wave_max_u32(~cand);  // wave minimum
+    if (lane_id() == 0) sh->red[wave_id()] = cand;
+    __syncthreads();
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int w = 0; w < TM_NWAVES; w++) best = sh->red[w] < best ? sh->red[w] : best;
+    __syncthreads();
+    if (best != 0xFFFFFFFFu) {
+        const uint16_t* old = b.fx_dlog + (s * dcap + (n - 1u - best) % dcap) * mac;
+        uint32_t diff = 0;
+        for (uint32_t k = threadIdx.x; k < na; k += TM_NT) diff |= old[k] != cells[k] ? 1u : 0u;
+        if (wg_sum(sh, diff) == 0) {
+            if (threadIdx.x == 0) sh->bytes += 2ull * na + 8ull * resident;
+            return true;  // the same set is logged already
+        }
+    }
+    if (n - f >= dcap) return false;
+    const size_t slot = s * dcap + n % dcap;
+    uint16_t* dst = b.fx_dlog + slot * mac;
     for (uint32_t k = threadIdx.x; k < na; k += TM_NT) dst[k] = cells[k];
     if (threadIdx.x == 0) {
-        b.fx_dlen[e] = (uint16_t)na;
-        b.fx_dn[t.s] = (uint32_t)slot + 1u;
-        sh->bytes += 2ull * na + 8ull;
+        b.fx_dlen[slot] = (uint16_t)na;
+        b.fx_dhash[slot] = h;
+        b.fx_dn[s] = n + 1u;
+        sh->bytes += 2ull * na + 8ull * resident + 8ull;
     }
     __syncthreads();
     return true;
@@ -3118,7 +3161,8 @@ int tm_configure_lds(const DevCfg& c) {
 // pairs, each with its own qualifying list.  Entries of one stream may run
 // concurrently: the writes store the value every replay computes.  The bytes
 // are not added to the streams' counters (the step kernel's roofline counts
-// its own work).  The host clears fx_fwork before and fx_dn after.
+// its own work).  The host clears fx_fwork before and sets fx_dflushed =
+// fx_dn after.
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
@@ -3130,8 +3174,11 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         const uint32_t j = __builtin_amdgcn_readfirstlane(job);
         if (j >= total) break;
         const int s = (int)(j / (uint32_t)c.fx_dcap);
-        const uint32_t e = j % (uint32_t)c.fx_dcap;
-        if (e >= b.fx_dn[s]) continue;
+        const uint32_t i = j % (uint32_t)c.fx_dcap;  // ring slot: entry n - 1 - d, d = (n - 1 - i) mod dcap
+        const uint32_t n = b.fx_dn[s], f = b.fx_dflushed[s];
+        if (n == f) continue;
+        const uint32_t d = (n - 1u + (uint32_t)c.fx_dcap - i % (uint32_t)c.fx_dcap) % (uint32_t)c.fx_dcap;
+        if (d > n - 1u - f) continue;  // slot holds no unflushed entry
         Tm t;
         tm_bind<false, true>(t, c, b, s, s, lds);
         t.q1 = b.fx_fq + (size_t)blockIdx.x * c.q_cap;
@@ -3144,7 +3191,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         }
         wg_clear(t.infA, c.cw);
         __syncthreads();
-        const size_t ei = (size_t)s * c.fx_dcap + e;
+        const size_t ei = (size_t)s * c.fx_dcap + i;
         const uint32_t len = b.fx_dlen[ei];
         const uint16_t* cl = b.fx_dlog + ei * (size_t)c.max_act_cells;
         for (uint32_t k = threadIdx.x; k < len; k += TM_NT) atomicOr(&t.infA[cl[k] >> 5], 1u << (cl[k] & 31));
