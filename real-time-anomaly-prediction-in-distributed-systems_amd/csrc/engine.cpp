@@ -602,10 +602,8 @@ static int alloc_fx(htm_engine* e) {
 // on `st`).  Called before anything reads or rebuilds the segment records.
 static int flush_deferred(htm_engine* e, hipStream_t st) {
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
-    HIP_TRY(hipMemsetAsync(e->tm.fx_fwork, 0, 4, st));
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, st))
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, st))  // (kernels only: no copy-engine work in the step stream)
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
-    HIP_TRY(hipMemcpyAsync(e->tm.fx_dflushed, e->tm.fx_dn, (size_t)e->n * 4, hipMemcpyDeviceToDevice, st));
     e->defer_steps = 0;
     return HTM_OK;
 }
@@ -712,11 +710,11 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, bt, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
+    if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
     if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : e->dc.fx_dcap / 2)) {
         int r = flush_deferred(e, st);
         if (r) return r;
     }
-    if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
 }
 

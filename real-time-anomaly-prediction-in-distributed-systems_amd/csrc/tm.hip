@@ -3161,8 +3161,8 @@ int tm_configure_lds(const DevCfg& c) {
 // pairs, each with its own qualifying list.  Entries of one stream may run
 // concurrently: the writes store the value every replay computes.  The bytes
 // are not added to the streams' counters (the step kernel's roofline counts
-// its own work).  The host clears fx_fwork before and sets fx_dflushed =
-// fx_dn after.
+// its own work).  tm_fx_flush_done_kernel then marks the entries flushed and
+// clears fx_fwork (zero at allocation) for the next flush.
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
@@ -3207,6 +3207,13 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
     }
 }
 
+// after a flush: every logged entry is flushed; the work counter restarts
+__global__ void tm_fx_flush_done_kernel(TmBufs b, int n) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) b.fx_dflushed[s] = b.fx_dn[s];
+    if (s == 0) *b.fx_fwork = 0u;
+}
+
 int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
     if (n <= 0 || !b.fx_dlog) return 0;
     const size_t lds = tm_step_lds_bytes(c, 0, 1);
@@ -3214,6 +3221,7 @@ int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) 
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
+    hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -305,6 +305,7 @@ def test_backtrack_assist_equals_serial_backtracks(rt, trained, traces):
         e.replicate(0)
         e.set_learning(False, False)
         e.set_option(rt._lib.OPT_BT_ASSIST, assist)
+        e.defer_duty(False)  # (assisted launches never defer: compare like with like)
         engs.append(e)
     rng = np.random.default_rng(17)
     idx = (np.arange(T)[:, None] + 97 * np.arange(n)[None, :]) % len(traces["test"])
