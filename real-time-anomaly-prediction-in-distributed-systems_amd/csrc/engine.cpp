@@ -73,6 +73,7 @@ struct htm_engine {
     int32_t profile = 0;
     std::vector<hipEvent_t> ev_pool;
     std::vector<int32_t> ev_steps;  // steps covered by each profiled event triple
+    std::vector<char> ev_fused;     // the triple's first event is unused (fused launch: no SP kernel)
     size_t ev_used = 0;
     int32_t fused = 1;              // HTM_OPT_FUSED
     int32_t run_chunk = 256;        // steps per fused htm_run launch
@@ -545,6 +546,7 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         e->profile = value ? 1 : 0;
         e->ev_used = 0;
         e->ev_steps.clear();
+        e->ev_fused.clear();
     }
     else if (opt == HTM_OPT_FUSED) {
         if (value && e->dc.sdr_in) return htm_fail(HTM_E_INVALID, "SDR-input engines run unfused");
@@ -652,6 +654,7 @@ static int next_events(htm_engine* e, hipEvent_t* ev, int32_t steps) {
     for (int k = 0; k < 3; k++) ev[k] = e->ev_pool[e->ev_used + k];
     e->ev_used += 3;
     e->ev_steps.push_back(steps);
+    e->ev_fused.push_back(0);
     return HTM_OK;
 }
 
@@ -683,7 +686,9 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     if (e->profile) {
         int r = next_events(e, ev, n_steps);
         if (r) return r;
-        HIP_TRY(hipEventRecord(ev[0], st));
+        // one event before and one after the fused kernel (an event record is
+        // a few microseconds of the queue's time: no empty "SP" interval)
+        e->ev_fused.back() = 1;
         HIP_TRY(hipEventRecord(ev[1], st));
     }
     // auto unit: a stream keeps its TM state in LDS for a unit's steps; longer
@@ -784,7 +789,7 @@ int htm_profile_read(htm_engine* e, double* out4) {
     double sp = 0.0, tm = 0.0;
     for (size_t k = 0; k + 2 < e->ev_used + 1 && k < e->ev_used; k += 3) {
         float a = 0.f, b = 0.f;
-        HIP_TRY(hipEventElapsedTime(&a, e->ev_pool[k], e->ev_pool[k + 1]));
+        if (!e->ev_fused[k / 3]) HIP_TRY(hipEventElapsedTime(&a, e->ev_pool[k], e->ev_pool[k + 1]));
         HIP_TRY(hipEventElapsedTime(&b, e->ev_pool[k + 1], e->ev_pool[k + 2]));
         sp += a;
         tm += b;
@@ -797,6 +802,7 @@ int htm_profile_read(htm_engine* e, double* out4) {
     out4[3] = (double)(e->ev_used / 3);
     e->ev_used = 0;
     e->ev_steps.clear();
+    e->ev_fused.clear();
     return HTM_OK;
 }
 
