@@ -54,6 +54,8 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
     int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
     uint32_t fx_n, fx_f; // deferred log: entries logged, entries flushed (thread 0's copies)
+    uint32_t p1_off;    // LDS offset of the active columns (ascending) phase 1 built infA from
+    int32_t p1_n;       // their number, or -1 when infA is not phase 1's
     float tf[4];
     uint32_t red[3 * TM_NWAVES];
     uint16_t act[HTM_MAXACT];
@@ -282,6 +284,10 @@ __device__ __forceinline__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, ui
 // _inferPhase1(activeColumns, useStartCells)
 __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start) {
     const int K = t.c.K;
+    if (threadIdx.x == 0) {  // (collect_frozen lists the active cells column by column)
+        t.sh->p1_off = (uint32_t)(reinterpret_cast<const char*>(cols) - reinterpret_cast<const char*>(t.sh));
+        t.sh->p1_n = nA;
+    }
     wg_clear(t.infA, t.c.cw);
     __syncthreads();
     uint32_t npc = 0;
@@ -544,6 +550,28 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
     uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
     uint32_t na;
     if (mode == FX_WIN_REUSE) {
+        na = (uint32_t)sh->fx_na;
+    } else if (sh->p1_n >= 0 && sh->p1_n <= 64) {
+        // infA is phase 1's: each active column's cells (ascending columns,
+        // ascending cells = the bitmap's order), listed by wave 0, one lane per column
+        if (wave_id() == 0) {
+            const int a = lane_id();
+            const int K = c.K;
+            const int p1n = sh->p1_n;
+            const uint16_t* p1c = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(sh) + sh->p1_off);
+            const uint32_t col = a < p1n ? p1c[a] : 0u;
+            const uint32_t f = a < p1n ? bm_field(t.infA, col * (uint32_t)K, (uint32_t)K) : 0u;
+            const uint32_t n1 = (uint32_t)__popc(f);
+            const uint32_t incl = wave_incl_scan(n1);
+            uint32_t pos = incl - n1;
+            for (uint32_t x = f; x; x &= x - 1) {
+                if (pos < mac) cells[pos] = (uint16_t)(col * (uint32_t)K + (uint32_t)(__ffs(x) - 1));
+                pos++;
+            }
+            const uint32_t tot = __shfl(incl, 63, 64);
+            if (a == 0) sh->fx_na = (int32_t)(tot < mac ? tot : mac);
+        }
+        __syncthreads();
         na = (uint32_t)sh->fx_na;
     } else {
         const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
@@ -1370,6 +1398,7 @@ __device__ __forceinline__ void infer_backtrack_assisted(Tm& t, int numPrev, uin
             if (inSeq) {
                 const uint32_t* rs = b.bt_res + (s * HTM_MAXPAT + start) * rw;
                 wg_copy(t.infA, rs, cw);
+                if (threadIdx.x == 0) sh->p1_n = -1;  // (infA is no longer phase 1's)
                 wg_copy(t.infP, rs + cw, cw);
                 wg_copy(reinterpret_cast<uint32_t*>(t.colconf), rs + 2 * cw, c.ncol);
             }
@@ -1387,6 +1416,7 @@ __device__ __forceinline__ void infer_backtrack_assisted(Tm& t, int numPrev, uin
                            __HIP_MEMORY_SCOPE_AGENT);
     if (candStart < 0) {
         wg_copy(t.infA, bkA, cw);
+        if (threadIdx.x == 0) sh->p1_n = -1;
         __syncthreads();
         (void)infer_phase2<FROZEN>(t);
     }
@@ -2322,6 +2352,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     tm_bind<LEARN, FROZEN>(t, c, b, s, s, lds);
     t.bt_epoch = bt_epoch;
     TmSh* sh = t.sh;
+    if (threadIdx.x == 0) sh->p1_n = -1;  // (no phase 1 yet this step)
 #ifdef HTM_STAMPS
     if (threadIdx.x == 0) {
         for (int k = 0; k < HTM_NSTAMP; k++) sh->st_acc[k] = sh->st_cnt[k] = 0;
@@ -3188,6 +3219,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
             sh->qn = 0;
             sh->bytes = 0;
             sh->lrn_iter = b.hdr[s].lrn_iter;  // frozen while TM learning is off
+            sh->p1_n = -1;                      // infA comes from the log, not from a phase 1
         }
         wg_clear(t.infA, c.cw);
         __syncthreads();
