@@ -149,24 +149,20 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
 #define HTM_OPT_RUN_UNIT 7      /* steps per work-queue unit of a fused htm_run launch (0, the
                                    default: launch steps / 8 clamped to [16, 64]); a stream's
                                    TM state stays in LDS for a unit's steps */
-#define HTM_OPT_BT_ASSIST 8     /* 0 (default) off; 1: in frozen lockstep launches (htm_step), up to 64
-                                   workgroups that finished their own stream replay other streams'
-                                   backtrack start offsets in parallel; 2: the owners run every offset
-                                   through the assisted path themselves.  Results are identical to
-                                   the serial loop in every mode (measured: no faster) */
-#define HTM_OPT_BT_TAIL 9       /* helpers join a launch's backtracks once at most this many owners are
-                                   still running (default 64) */
+/* 8, 9: retired (round-2 backtrack assist, measured no faster; removed from the kernels) */
 #define HTM_OPT_DEFER_DUTY 10   /* 1 (default): in frozen lockstep steps (htm_step), a phase 2 whose
                                    confidences the step discards (backtrack replays, out-of-sequence
                                    results) computes only the predicted cells; the first dutyCycle()
                                    record write of its qualifying segments is deferred to a flush kernel
-                                   (every 32 steps, and before any call that reads the records: export,
-                                   save, learning on, htm_status / htm_counters, htm_flush).  Results and
+                                   that runs on the engine's own HIP stream beside the next steps (every
+                                   8 steps), and completes before any call that reads the records: export,
+                                   save, learning on, htm_status / htm_counters, htm_flush.  Results and
                                    state are those of the undeferred step.  0: count every phase 2 in full */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
-/* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY) on `stream`
- * (asynchronous): a benchmark's timed region ends with it. */
+/* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued
+ * on `stream` afterwards sees them (asynchronous w.r.t. the host); a
+ * benchmark's timed region ends with it. */
 int htm_flush(htm_engine* eng, void* stream);
 
 /* Kernel times of the profiled launches since the last call (synchronises):

@@ -43,8 +43,6 @@ OPT_PROFILE = 4
 OPT_FUSED = 5
 OPT_RUN_CHUNK = 6
 OPT_RUN_UNIT = 7
-OPT_BT_ASSIST = 8
-OPT_BT_TAIL = 9
 OPT_DEFER_DUTY = 10
 
 

@@ -79,17 +79,25 @@ struct htm_engine {
     int32_t run_chunk = 256;        // steps per fused htm_run launch
     int32_t run_unit = 0;           // steps per work unit of the fused kernel's queue (0: auto)
     uint32_t* wq = nullptr;         // the fused kernel's work queue: next unit + per-stream done blocks
-    int32_t bt_assist = 0;          // HTM_OPT_BT_ASSIST (needs the bt_* buffers); off by default:
-                                    // measured no faster on config 2 (profiles/r02_assist/ab.json)
-    int32_t bt_tail = 64;           // HTM_OPT_BT_TAIL: owners left when helpers join
-    uint32_t bt_epoch = 0;          // last assisted launch's tag
-    unsigned long long bt_base = 0; // workgroups counted by bt_ctl before the next assisted launch
     int32_t defer = 1;              // HTM_OPT_DEFER_DUTY: frozen lockstep steps defer discarded phase 2s' duty writes
     int32_t defer_steps = 0;        // lockstep launches since the last flush of the deferred log
-    int32_t flush_every = 0;        // lockstep launches between flushes (0: fx_dcap / 2)
+    int32_t flush_every = 0;        // lockstep launches between flushes (0: FLUSH_EVERY)
+    // the flush of the deferred log runs on its own stream, concurrently with
+    // the next steps (they never read the records it writes): a snapshot of
+    // the log counters on the step stream, the flush on fstream after it
+    hipStream_t fstream = nullptr;
+    hipEvent_t ev_logged = nullptr;   // step stream: the snapshot of the log counters
+    hipEvent_t ev_flushed = nullptr;  // fstream: the last enqueued flush is complete
+    bool flush_pending = false;       // ev_flushed not yet waited for by a step stream or the host
 };
 
+// lockstep launches between two flushes of the deferred log (the flush runs
+// beside the steps, so frequent small flushes keep the one a timed region or
+// a state read must wait for short)
+#define FLUSH_EVERY 8
+
 static int flush_deferred(htm_engine* e, hipStream_t st);
+static int flush_sync(htm_engine* e);
 
 extern "C" {
 
@@ -351,28 +359,6 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.colnz, uint32_t, S * ((size_t)d.nw + 1));
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
-    // backtrack assist buffers (frozen lockstep launches): ~16 x 14 KB per
-    // stream of replay results; left out for very large engines (fleets of
-    // 100K+ streams amortise their backtracks over the launch instead)
-    {
-        const size_t rw = 2 * (size_t)d.cw + (size_t)d.ncol;
-        const size_t per = HTM_MAXPAT * (rw * 4 + 16 + 8 + HTM_MAXACT * 2) + 16 + BT_INFO_WORDS * 4;
-        if (S * per <= ((size_t)4 << 30)) {
-            ALLOC(e->tm.bt_state, unsigned long long, S);
-            ALLOC(e->tm.bt_take, unsigned long long, S);
-            ALLOC(e->tm.bt_claim, unsigned long long, S * HTM_MAXPAT);
-            ALLOC(e->tm.bt_res, uint32_t, S * HTM_MAXPAT * rw);
-            ALLOC(e->tm.bt_meta, uint32_t, S * HTM_MAXPAT * 4);
-            ALLOC(e->tm.bt_pat, uint16_t, S * HTM_MAXPAT * HTM_MAXACT);
-            ALLOC(e->tm.bt_info, uint32_t, S * BT_INFO_WORDS);
-            ALLOC(e->tm.bt_ctl, unsigned long long, 4);
-        } else {
-            e->tm.bt_state = nullptr;
-            e->tm.bt_take = e->tm.bt_claim = e->tm.bt_ctl = nullptr;
-            e->tm.bt_res = e->tm.bt_meta = e->tm.bt_info = nullptr;
-            e->tm.bt_pat = nullptr;
-        }
-    }
 #ifdef HTM_STAMPS
     ALLOC(e->tm.dbg, uint64_t, S * 2 * HTM_NSTAMP);
 #endif
@@ -516,13 +502,16 @@ int htm_destroy(htm_engine* e) {
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->tm.fx_ent) (void)hipFree(e->tm.fx_ent);
     for (hipEvent_t x : e->ev_pool) (void)hipEventDestroy(x);
+    if (e->ev_logged) (void)hipEventDestroy(e->ev_logged);
+    if (e->ev_flushed) (void)hipEventDestroy(e->ev_flushed);
+    if (e->fstream) (void)hipStreamDestroy(e->fstream);
     delete e;
     return HTM_OK;
 }
 
 int htm_set_learning(htm_engine* e, int32_t sp_learn, int32_t tm_learn) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
-    if (int r = flush_deferred(e, nullptr)) return r;
+    if (int r = flush_sync(e)) return r;
     if (e->fleet && (sp_learn || tm_learn))
         return htm_fail(HTM_E_STATE, "a fleet engine shares one frozen model: learning stays off");
     e->sp_learn = sp_learn ? 1 : 0;
@@ -558,12 +547,10 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
     }
     else if (opt == HTM_OPT_DEFER_DUTY) {
         if (!value) {
-            if (int r = flush_deferred(e, nullptr)) return r;
+            if (int r = flush_sync(e)) return r;
         }
         e->defer = value ? 1 : 0;
     }
-    else if (opt == HTM_OPT_BT_ASSIST) e->bt_assist = value < 0 ? 0 : value > 2 ? 2 : value;
-    else if (opt == HTM_OPT_BT_TAIL) e->bt_tail = value < 0 ? 0 : value > 0xFFFFFF ? 0xFFFFFF : value;
     else if (opt == HTM_OPT_RUN_UNIT) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
         e->run_unit = value;
@@ -587,34 +574,86 @@ static int alloc_fx(htm_engine* e) {
     ALLOC(e->tm.fx_nr, uint32_t, M);
     ALLOC(e->tm.fx_pcell, uint16_t, M * (size_t)d.fx_pcap);
     ALLOC(e->tm.fx_np, uint32_t, M);
-    // deferred dutyCycle() writes of lockstep steps: a log per stream, the
-    // flush kernel's per-workgroup qualifying lists
+    return HTM_OK;
+}
+
+// The deferred dutyCycle() log of lockstep steps (a ring per stream), the
+// flush kernel's per-workgroup qualifying lists, and the flush stream:
+// allocated on the first deferring launch, so engines that never step frozen
+// in lockstep (learning, htm_run replays, HTM_OPT_DEFER_DUTY 0) do not pay.
+static int alloc_dlog(htm_engine* e) {
+    if (e->tm.fx_dlog) return HTM_OK;
+    const DevCfg& d = e->dc;
     const size_t S = (size_t)e->n;
-    ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * (size_t)d.max_act_cells);
     ALLOC(e->tm.fx_dlen, uint16_t, S * (size_t)d.fx_dcap);
     ALLOC(e->tm.fx_dhash, uint32_t, S * (size_t)d.fx_dcap);
     ALLOC(e->tm.fx_dn, uint32_t, S);
     ALLOC(e->tm.fx_dflushed, uint32_t, S);
+    ALLOC(e->tm.fx_dsnap, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
-    ALLOC(e->tm.fx_fwork, uint32_t, 1);
+    ALLOC(e->tm.fx_fwork, uint32_t, 2);
+    HIP_TRY(hipStreamCreateWithFlags(&e->fstream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_logged, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_flushed, hipEventDisableTiming));
+    ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * (size_t)d.max_act_cells);  // last: the "allocated" test
     return HTM_OK;
 }
 
-// Replay the deferred dutyCycle() writes logged by lockstep steps (asynchronous
-// on `st`).  Called before anything reads or rebuilds the segment records.
-static int flush_deferred(htm_engine* e, hipStream_t st) {
+// Flush of the deferred dutyCycle() writes logged by lockstep steps.
+// flush_async: snapshot the log counters on the step stream `st` (the entries
+// logged so far), then replay those entries on the flush stream, which waits
+// for the snapshot only -- later steps run beside the flush (they append to
+// the ring's free slots and never read the segment records it writes).
+static int flush_async(htm_engine* e, hipStream_t st) {
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, st))  // (kernels only: no copy-engine work in the step stream)
+    if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
+    HIP_TRY(hipEventRecord(e->ev_logged, st));
+    HIP_TRY(hipStreamWaitEvent(e->fstream, e->ev_logged, 0));
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->fstream))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipEventRecord(e->ev_flushed, e->fstream));
     e->defer_steps = 0;
+    e->flush_pending = true;
+    return HTM_OK;
+}
+
+// Flush and order `st` after it: work enqueued on `st` afterwards sees every
+// record write of the steps enqueued before (stream-ordered, asynchronous).
+static int flush_deferred(htm_engine* e, hipStream_t st) {
+    if (int r = flush_async(e, st)) return r;
+    if (e->flush_pending) {
+        HIP_TRY(hipStreamWaitEvent(st, e->ev_flushed, 0));
+        e->flush_pending = false;
+    }
+    return HTM_OK;
+}
+
+// Host-side flush before the host reads or replaces the state: every stream
+// of the device is drained first (the steps may have been issued on any
+// stream, e.g. torch's current one), then the flush runs to completion.
+static int flush_sync(htm_engine* e) {
+    if (!e->tm.fx_dlog) return HTM_OK;
+    HIP_TRY(hipDeviceSynchronize());
+    if (e->defer_steps) {
+        if (int r = flush_async(e, e->fstream)) return r;
+        HIP_TRY(hipStreamSynchronize(e->fstream));
+    }
+    e->flush_pending = false;
     return HTM_OK;
 }
 
 static int build_fx(htm_engine* e, hipStream_t st) {
     const DevCfg& d = e->dc;
-    int ra = flush_deferred(e, st);  // the log refers to the index being replaced
+    int ra = flush_sync(e);  // the log refers to the index being replaced
     if (!ra) ra = alloc_fx(e);
     if (ra) return ra;
+    if (e->tm.fx_dlog) {
+        // the logged sets were recorded against the old records and iteration:
+        // an empty ring, so no later set is taken for one already written
+        HIP_TRY(hipMemsetAsync(e->tm.fx_dn, 0, (size_t)e->n * 4, st));
+        HIP_TRY(hipMemsetAsync(e->tm.fx_dflushed, 0, (size_t)e->n * 4, st));
+        HIP_TRY(hipMemsetAsync(e->tm.fx_dsnap, 0, (size_t)e->n * 4, st));
+    }
     if (launch_tm_fx_rank(d, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "fx rank launch");
     if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return htm_fail(HTM_E_HIP, "fx count launch");
     std::vector<uint64_t> counts((size_t)e->nm);
@@ -696,28 +735,21 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     // the launch's tail (measured on config 2, profiles/r01_s4/ab_unit.txt:
     // 256-step launches best at 32, 2324-step launches flat over 48..96)
     const int32_t unit = e->run_unit > 0 ? e->run_unit : std::max(16, std::min(64, n_steps / 8));
-    // backtrack assist: frozen one-step (lockstep) launches; the kernel counts
-    // its workgroups in bt_ctl on top of `base`
-    BtArgs bt{};
     TmBufs tb = e->tm;
-    if (frozen && n_steps == 1 && e->bt_assist && e->tm.bt_state) {
-        bt.epoch = ++e->bt_epoch;
-        // helpers (1) join once at most bt_tail owners are left; 2: owners only (A/B)
-        bt.pad = e->bt_assist == 1 ? (1u | ((uint32_t)e->bt_tail << 8)) : 0u;
-        bt.base = e->bt_base;
-        e->bt_base += (unsigned long long)e->n;
+    // deferred dutyCycle() writes: frozen lockstep launches (one step)
+    const bool defer = frozen && n_steps == 1 && e->defer;
+    if (defer) {
+        if (int r = alloc_dlog(e)) return r;
+        tb = e->tm;
     } else {
-        tb.bt_state = nullptr;  // the kernel's "off" test
+        tb.fx_dlog = nullptr;
     }
-    // deferred dutyCycle() writes: frozen lockstep launches (one step), not assisted
-    const bool defer = frozen && n_steps == 1 && e->defer && tb.fx_dlog && !tb.bt_state;
-    if (!defer) tb.fx_dlog = nullptr;
     if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
-                       e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, bt, st))
+                       e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
-    if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : e->dc.fx_dcap / 2)) {
-        int r = flush_deferred(e, st);
+    if (defer && ++e->defer_steps >= std::min(e->flush_every ? e->flush_every : FLUSH_EVERY, e->dc.fx_dcap / 2)) {
+        int r = flush_async(e, st);  // beside the next steps
         if (r) return r;
     }
     return HTM_OK;
@@ -806,12 +838,19 @@ int htm_profile_read(htm_engine* e, double* out4) {
     return HTM_OK;
 }
 
+// error flags of the deferred-duty flushes (host; the device is idle)
+static uint32_t flush_error(htm_engine* e) {
+    uint32_t x = 0;
+    if (e->tm.fx_fwork && hipMemcpy(&x, e->tm.fx_fwork + 1, 4, hipMemcpyDeviceToHost) != hipSuccess) x = 0;
+    return x;
+}
+
 // Sum of the per-stream TM counters: out8 = {algorithmic bytes, inferPhase2
 // calls, inferBacktracks, learnPhase2 calls, learnBacktracks, live segments,
 // pool high-water marks, OR of error flags}
 int htm_counters(htm_engine* e, uint64_t* out8) {
     if (!e || !out8) return htm_fail(HTM_E_INVALID, "bad arguments");
-    if (int r = flush_deferred(e, nullptr)) return r;
+    if (int r = flush_sync(e)) return r;
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
@@ -819,6 +858,7 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
     std::vector<uint32_t> spe((size_t)e->n);
     HIP_TRY(hipMemcpy(spe.data(), e->sp.err, spe.size() * 4, hipMemcpyDeviceToHost));
     for (uint32_t x : spe) out8[7] |= x;
+    out8[7] |= flush_error(e);
     for (const auto& x : h) {
         out8[0] += x.stat_bytes;
         out8[1] += x.stat_inf_phase2;
@@ -1057,7 +1097,7 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
         return htm_fail(HTM_E_INVALID, "bad export arguments");
     const Region& r = e->regions[region];
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "export buffer too small");
-    if (int rf = flush_deferred(e, nullptr)) return rf;
+    if (int rf = flush_sync(e)) return rf;
     HIP_TRY(hipDeviceSynchronize());
     if (r.per_stream == 0) return HTM_OK;
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_export(e, s0, n, h_dst, nullptr);
@@ -1085,7 +1125,7 @@ static int import_region(htm_engine* e, int32_t region, int32_t s0, int32_t n, c
     // no checkpoints (an export of a dense engine): the streams keep their own
     if (region == HTM_ST_SP_PERM_CKPT && (bytes == 0 || r.per_stream == 0)) return HTM_OK;
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "import buffer too small");
-    if (int rf = flush_deferred(e, nullptr)) return rf;
+    if (int rf = flush_sync(e)) return rf;
     HIP_TRY(hipDeviceSynchronize());
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_import(e, s0, n, h_src, nullptr, 0);
     if (rebase && e->dc.sp_paged && (region == HTM_ST_SP_PERM_CKPT || region == HTM_ST_SP_POTMASK))
@@ -1135,7 +1175,7 @@ static int replicate_region(uint8_t* base, size_t per, int32_t src, int32_t n, h
 int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     if (!e || src < 0 || src >= e->n) return htm_fail(HTM_E_INVALID, "bad source stream");
     hipStream_t st = (hipStream_t)stream;
-    if (int rf = flush_deferred(e, st)) return rf;
+    if (int rf = flush_sync(e)) return rf;
     for (int id = 1; id <= HTM_ST_COUNT; id++) {
         const Region& r = e->regions[id];
         if (!r.base || !r.per_stream) continue;
@@ -1172,7 +1212,7 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
     if (model_stream < 0 || model_stream >= model->n) return htm_fail(HTM_E_INVALID, "bad model stream");
     *out = nullptr;
     HIP_TRY(hipSetDevice(model->device));
-    if (int rf = flush_deferred(const_cast<htm_engine*>(model), nullptr)) return rf;
+    if (int rf = flush_sync(const_cast<htm_engine*>(model))) return rf;
     HIP_TRY(hipDeviceSynchronize());
     htm_engine* e = nullptr;
     htm_config fcfg = model->cfg;
@@ -1247,12 +1287,15 @@ int32_t htm_abi_version(void) { return HTM_ABI_VERSION; }
 // Synchronise and report per-stream error flags (pool/queue overflow).
 int htm_status(htm_engine* e) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
-    if (int r = flush_deferred(e, nullptr)) return r;
+    if (int r = flush_sync(e)) return r;
     HIP_TRY(hipDeviceSynchronize());
     std::vector<htm_tm_header> h((size_t)e->n);
     HIP_TRY(hipMemcpy(h.data(), e->tm.hdr, h.size() * sizeof(htm_tm_header), hipMemcpyDeviceToHost));
     std::vector<uint32_t> spe((size_t)e->n);
     HIP_TRY(hipMemcpy(spe.data(), e->sp.err, spe.size() * 4, hipMemcpyDeviceToHost));
+    if (uint32_t fe = flush_error(e))
+        return htm_fail(HTM_E_CAPACITY, "deferred-duty flush error flags 0x%x (16: qualifying-segment list overflow, "
+                        "results invalid -- raise q_capacity)", fe);
     for (int s = 0; s < e->n; s++) {
         if (spe[s] & SP_ERR_POOL)
             return htm_fail(HTM_E_CAPACITY, "stream %d error flag 0x20: SP permanence row pool exhausted -- updates "

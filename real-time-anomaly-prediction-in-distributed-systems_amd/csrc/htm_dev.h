@@ -144,19 +144,6 @@ struct TmBufs {
     uint16_t* fx_pcell;     // [S][fx_pcap] cell of each pid
     uint32_t* fx_np;        // [S] number of pids (> fx_pcap: pid lists not built, rows are read)
     uint64_t* dbg;          // [S][32] phase stamps + event counts (HTM_STAMPS builds only, else null)
-    // backtrack assist (frozen lockstep launches): a stream whose step needs
-    // _inferBacktrack posts its pattern history; workgroups that finished
-    // their own stream replay other start offsets of posted jobs in parallel
-    // (the replays are independent while the TM is frozen); the owner takes
-    // the first in-sequence start in NuPIC's order.  Null when not allocated.
-    unsigned long long* bt_state;  // [S] job word: epoch << 16 | numPrev (BT_CLOSED: done)
-    unsigned long long* bt_take;   // [S] next start a helper takes: epoch << 16 | k
-    unsigned long long* bt_claim;  // [S][HTM_MAXPAT] epoch << 2 | 1 claimed, 2 done in sequence, 3 done failed
-    uint32_t* bt_res;              // [S][HTM_MAXPAT][2 * cw + ncol] infA, infP, colConfidence of an in-sequence replay
-    uint32_t* bt_meta;             // [S][HTM_MAXPAT][4] replay's bytes (lo, hi), phase-2 calls, error flags
-    uint16_t* bt_pat;              // [S][HTM_MAXPAT][HTM_MAXACT] posted pattern history (oldest first)
-    uint32_t* bt_info;             // [S][BT_INFO_WORDS] numPrev, lrn_iter, avg density (2 words), lengths
-    unsigned long long* bt_ctl;    // [3] workgroups started, owners done, helper slots taken (monotonic)
     // Deferred dutyCycle() writes (frozen lockstep launches; null: off).  A
     // frozen phase 2 whose confidences the step discards needs only the
     // predicted cells (the pid pass) for what follows; its one remaining effect,
@@ -168,23 +155,14 @@ struct TmBufs {
     uint32_t* fx_dhash;            // [S][fx_dcap] hash of the set
     uint32_t* fx_dn;               // [S] entries logged (monotonic)
     uint32_t* fx_dflushed;         // [S] entries flushed
+    uint32_t* fx_dsnap;            // [S] fx_dn when the running flush was enqueued (its upper bound)
     uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
-    uint32_t* fx_fwork;            // [1] flush work counter
+    uint32_t* fx_fwork;            // [2] flush work counter, flush error flags (16: qualifying-list overflow)
 };
 
 #define FX_FLUSH_WG 1024  // persistent workgroups of tm_fx_flush_kernel (each has its own scratch list)
 
-#define BT_INFO_WORDS (4 + HTM_MAXPAT)
 #define FX_FRESH 0x80000000u  // fx_rec.x: the segment's dutyCycle record holds its frozen value
-#define BT_HELPERS 64  // finished workgroups that stay to help per launch
-#define BT_CLOSED 0xFFFFull
-
-// launch arguments of the backtrack assist (epoch 0: off)
-struct BtArgs {
-    uint32_t epoch;               // launch tag, > 0 and distinct per assisted launch
-    uint32_t pad;                 // bit 0: finished workgroups help (else owners replay every offset)
-    unsigned long long base;      // bt_ctl counts of the earlier assisted launches (n per launch)
-};
 
 // Diagnostic phase stamps (HTM_STAMPS builds only): thread 0 charges the
 // shader cycles since its previous stamp to bucket k.  Compiled out of the
@@ -376,10 +354,11 @@ int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* sc
                    int n, hipStream_t st);
 int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
                    int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
-                   uint32_t* wq, int unit_steps, BtArgs bt, hipStream_t st);
+                   uint32_t* wq, int unit_steps, hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen);

@@ -1,2839 +1,11 @@
-// tm.hip -- BacktrackingTM (TMRegion, temporalImp "cpp") + raw anomaly for
-// N streams on gfx950, one 256-thread workgroup per stream per step.
-//
-// Reference path: TMRegion.compute -> BacktrackingTMCPP.compute -> Cells4
-// (params ML/HTM/NetworkUtils.py:44-64,140-153; anomaly read at
-// ML/HTM/NetworkModel.py:133).  Control flow restates NuPIC's BacktrackingTM
-// (updateInferenceState / inferPhase1 / inferPhase2 / inferBacktrack,
-// updateLearningState / learnPhase1 / learnPhase2 / learnBacktrack,
-// processSegmentUpdates, adaptSegment, getBestMatchingCell,
-// getCellForNewSegment, chooseCellsToLearnFrom) exactly as oracle/htm_oracle.c
-// does.
-//
-// MI355X design:
-//   * the whole step of one stream runs inside one workgroup: its bitmaps
-//     (cells x 1 bit), column confidences and bookkeeping live in LDS;
-//     segment state streams from HBM;
-//   * inference phase 2 (the hot loop) has two forms with identical results:
-//       - learning on:  a coalesced scan of the segment pool (4 lanes per
-//         segment, 16 B of synapse sources each) probing the LDS bitmap;
-//       - learning off: forward propagation over a frozen cell -> segment
-//         index (what Cells4's _outSynapses does), counting active synapses
-//         per segment with LDS atomics in windows of the slot space, so a
-//         step reads only the out-synapses of the active cells;
-//   * the float32 column confidences are summed in NuPIC's (column, cell,
-//     segment) order (bucket sort of the qualifying segments), so they are
-//     bit-identical to the oracle;
-//   * the data-dependent nupic::Random draws of learning run on lane 0 of
-//     wave 0 in NuPIC order; everything else is wave- or workgroup-parallel.
-#include "sp_dev.h"
-
-
-
-__constant__ float kDcAlpha[9] = {0.0f, 0.0032f, 0.0010f, 0.00032f, 0.00010f, 0.000032f, 0.00001f, 0.0000032f, 0.0000010f};
-__constant__ uint32_t kDcTier[9] = {0, 100, 320, 1000, 3200, 10000, 32000, 100000, 320000};
-
-struct __attribute__((aligned(16))) TmSh {
-    double avg_dens, avg_lsl;
-    unsigned long long bytes;      // algorithmic HBM bytes of this step (thread 0 / LDS atomics)
-    unsigned long long bytes_acc;  // ... of the earlier steps of a run kept in LDS
-    uint32_t lrn_iter, iter;
-    int32_t pam, lsl, reset, have_avg;
-    uint32_t rng[31];
-    int32_t rf, rr;
-    uint32_t hwm, nlive;
-    int32_t n_inf_pat, n_lrn_pat, inf_head, lrn_head;
-    uint16_t inf_len[HTM_MAXPAT], lrn_len[HTM_MAXPAT];
-    int32_t n_upd;
-    uint32_t err;
-    uint32_t st[4];
-    int32_t nA;
-    int32_t qn;
-    int32_t ncand;
-    int32_t ti[8];
-    int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
-    int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
-    uint32_t fx_n, fx_f; // deferred log: entries logged, entries flushed (thread 0's copies)
-    uint32_t p1_off;    // LDS offset of the active columns (ascending) phase 1 built infA from
-    int32_t p1_n;       // their number, or -1 when infA is not phase 1's
-    float tf[4];
-    uint32_t red[3 * TM_NWAVES];
-    uint16_t act[HTM_MAXACT];
-    uint32_t cand[HTM_MAXACT];
-    uint32_t newsrc[HTM_MAXSYN];
-    uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
-#ifdef HTM_STAMPS
-    uint64_t st_acc[HTM_NSTAMP], st_cnt[HTM_NSTAMP], st_last, st_start;
-#endif
-};
-
-struct Tm {
-    DevCfg c;
-    int s;
-    TmSh* sh;
-    // LDS regions
-    uint32_t *infA, *infP, *infP1, *lrnA, *lrnA1, *lrnP, *lrnP1;
-    float* colconf;
-    uint32_t* flags;   // ncol bits
-    uint32_t* U;       // union region
-    uint16_t (*lrnpat)[HTM_MAXACT];  // learn-state pattern ring (learning layouts only)
-    // global, this stream
-    uint32_t* meta;
-    uint16_t* src;
-    float* perm;
-    uint32_t* conn;
-    uint32_t* duty;
-    uint8_t* nseg;
-    htm_tm_update* upd;
-    uint32_t* sbm;     // scratch bitmaps [5][cw]
-    float* sconf;
-    uint32_t* q1;
-    uint32_t* q2;
-    const uint32_t* fxoff;
-    const uint4* fxent;
-    const uint2* fxrec;
-    const uint32_t* fxrslot;
-    const uint16_t* fxpcell;
-    uint32_t np;       // predictive-capable segments (pids) of this stream
-    uint32_t nr;       // ranks (live segments) of the frozen index
-    const TmBufs* tb;  // the engine's buffers (backtrack assist)
-    uint32_t bt_epoch; // > 0: this launch's backtracks are assisted (frozen lockstep)
-    bool defer;        // discarded frozen phase 2s log their active cells (TmBufs::fx_dlog)
-};
-
-// stamp buckets (HTM_STAMPS): where one stream-step's cycles go
-enum {
-    SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR
-};
-// event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
-// and a histogram of whole-step cycles: SC_HIST + b counts steps of
-// [2^(15+b), 2^(16+b)) cycles (b = 0 also holds shorter ones, b = 8 longer)
-enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
-
-// ---------------------------------------------------------------------------
-// LDS layout
-struct TmLayout {
-    size_t off_lpat, off_bm, off_conf, off_flags, off_U, total;
-    int nbm;
-    size_t u_words;
-};
-
-__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-
-__host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int frozen) {
-    TmLayout L;
-    L.nbm = learn ? 7 : 3;
-    size_t o = align16(sizeof(TmSh));
-    L.off_lpat = o;  // the learn-state pattern ring: learning only
-    if (learn) o = align16(o + (size_t)HTM_MAXPAT * HTM_MAXACT * 2);
-    L.off_bm = o;
-    o = align16(o + (size_t)L.nbm * c.cw * 4);
-    L.off_conf = o;
-    o = align16(o + (size_t)c.ncol * 4);
-    L.off_flags = o;
-    o = align16(o + (size_t)c.nw * 4);
-    L.off_U = o;
-    // union of phase-local arrays:
-    //  finish: colcnt[ncol] u32, nzcol[ncol] u16, nzstart[ncol+1] u32, and the
-    //          qualifying-segment buffers qkey/qdc/skey/sdc[q_lds]
-    //  keys (learning): best-match keys u64[ncol]
-    //  frozen collection: u8 counters[fx_win], active cells u16[max_act_cells],
-    //          block prefix u32[max_act_cells+1], list starts u32[max_act_cells],
-    //          block -> list map u16[FX_OWN]
-    //  trim flags (learning): u32[upd_cap]
-    size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
-                 (size_t)(c.q_lds + 1) / 2 + (size_t)c.nw;
-    size_t keys = learn ? 2 * (size_t)c.ncol : 0;
-    size_t col = frozen ? (size_t)c.fx_win / 4 + 64 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
-                              1 + FX_OWN / 2
-                        : 0;
-    size_t trim = learn ? (size_t)c.upd_cap : 0;
-    size_t spw = (sizeof(SpShared) + 3) / 4;  // the fused kernels' SP step
-    size_t u = fin;
-    if (spw > u) u = spw;
-    if (keys > u) u = keys;
-    if (col > u) u = col;
-    if (trim > u) u = trim;
-    L.u_words = u;
-    o = align16(o + u * 4);
-    L.total = o;
-    return L;
-}
+// tm.hip -- host launchers of the TM kernels, the per-stream init / reset
+// kernels, the frozen-index build (rank / count / fill) and the deferred
+// dutyCycle() flush.  The step kernels themselves are in tm_k_*.hip, their
+// device code in tm_core.h (BacktrackingTM + raw anomaly, see its header).
+#include "tm_core.h"
 
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).total; }
 size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).off_U; }
-
-// ---------------------------------------------------------------------------
-// workgroup helpers
-__device__ __forceinline__ void wg_clear(uint32_t* p, int n) {
-    if ((((uintptr_t)p) & 15) == 0 && (n & 3) == 0) {
-        uint4* p4 = reinterpret_cast<uint4*>(p);
-        for (int i = threadIdx.x; i < (n >> 2); i += TM_NT) p4[i] = make_uint4(0u, 0u, 0u, 0u);
-    } else {
-        for (int i = threadIdx.x; i < n; i += TM_NT) p[i] = 0;
-    }
-}
-__device__ __forceinline__ void wg_copy(uint32_t* d, const uint32_t* s, int n) {
-    for (int i = threadIdx.x; i < n; i += TM_NT) d[i] = s[i];
-}
-// sum over the workgroup (contains barriers; call uniformly)
-__device__ __forceinline__ uint32_t wg_sum(TmSh* sh, uint32_t v) {
-    v = wave_sum_u32(v);
-    __syncthreads();
-    if (lane_id() == 0) sh->red[wave_id()] = v;
-    __syncthreads();
-    uint32_t t = 0;
-#pragma unroll
-    for (int w = 0; w < TM_NWAVES; w++) t += sh->red[w];
-    __syncthreads();
-    return t;
-}
-// The same with one barrier, through its own slots of sh->red: callers must
-// have passed another barrier since the previous call read them.
-__device__ __forceinline__ uint32_t wg_excl_scan1(TmSh* sh, uint32_t v, uint32_t* total);
-
-// exclusive prefix over the workgroup in thread order; *total gets the sum
-__device__ __forceinline__ uint32_t wg_excl_scan(TmSh* sh, uint32_t v, uint32_t* total) {
-    uint32_t incl = wave_incl_scan(v);
-    __syncthreads();
-    if (lane_id() == 63) sh->red[wave_id()] = incl;
-    __syncthreads();
-    uint32_t base = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < TM_NWAVES; w++) {
-        if (w < wave_id()) base += sh->red[w];
-        tot += sh->red[w];
-    }
-    __syncthreads();
-    *total = tot;
-    return base + incl - v;
-}
-
-__device__ __forceinline__ uint32_t wg_excl_scan1(TmSh* sh, uint32_t v, uint32_t* total) {
-    const uint32_t incl = wave_incl_scan(v);
-    if (lane_id() == 63) sh->red[2 * TM_NWAVES + wave_id()] = incl;
-    __syncthreads();
-    uint32_t base = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < TM_NWAVES; w++) {
-        const uint32_t x = sh->red[2 * TM_NWAVES + w];
-        if (w < (int)wave_id()) base += x;
-        tot += x;
-    }
-    *total = tot;
-    return base + incl - v;
-}
-
-__device__ __forceinline__ uint32_t col_of(const DevCfg& c, uint32_t cell) { return __umulhi(cell, c.kmagic); }
-__device__ __forceinline__ uint32_t kmask(int K) { return K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u); }
-
-// Segment::dutyCycle(iteration, active, readOnly=false) on the pool entry
-__device__ __forceinline__ float seg_dc_update(uint32_t* duty, uint32_t slot, uint32_t it, bool active) {
-    uint32_t* d = duty + (size_t)slot * 3;
-    float dc;
-    if (it <= kDcTier[1]) {
-        dc = (float)d[0] / (float)it;
-        d[1] = __float_as_uint(dc);
-        d[2] = it;
-        return dc;
-    }
-    uint32_t age = it - d[2];
-    float last = __uint_as_float(d[1]);
-    if (age == 0 && !active) return last;
-    float alpha = 0.0f;
-    for (int t = 8; t > 0; t--) {
-        if (it > kDcTier[t]) { alpha = kDcAlpha[t]; break; }
-    }
-    dc = pow_det((float)(1.0 - (double)alpha), age) * last;
-    if (active) dc += alpha;
-    d[1] = __float_as_uint(dc);
-    d[2] = it;
-    return dc;
-}
-
-// ---------------------------------------------------------------------------
-// cell list of a bitmap (ascending) into dst; returns count (uniform)
-__device__ __forceinline__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, uint32_t* dst32, uint16_t* dst16, uint32_t cap) {
-    const int cw = t.c.cw;
-    const int per = (cw + TM_NT - 1) / TM_NT;
-    const int w0 = threadIdx.x * per;
-    uint32_t cnt = 0;
-    for (int k = 0; k < per; k++)
-        if (w0 + k < cw) cnt += __popc(bm[w0 + k]);
-    uint32_t total;
-    uint32_t pos = wg_excl_scan(t.sh, cnt, &total);
-    for (int k = 0; k < per; k++) {
-        int w = w0 + k;
-        if (w >= cw) break;
-        for (uint32_t x = bm[w]; x; x &= x - 1) {
-            uint32_t cell = (uint32_t)w * 32 + __ffs(x) - 1;
-            if (pos < cap) {
-                if (dst32) dst32[pos] = cell;
-                if (dst16) dst16[pos] = (uint16_t)cell;
-            }
-            pos++;
-        }
-    }
-    __syncthreads();
-    return total;
-}
-
-// ---------------------------------------------------------------------------
-// Inference
-// _inferPhase1(activeColumns, useStartCells)
-__device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start) {
-    const int K = t.c.K;
-    if (threadIdx.x == 0) {  // (collect_frozen lists the active cells column by column)
-        t.sh->p1_off = (uint32_t)(reinterpret_cast<const char*>(cols) - reinterpret_cast<const char*>(t.sh));
-        t.sh->p1_n = nA;
-    }
-    wg_clear(t.infA, t.c.cw);
-    __syncthreads();
-    uint32_t npc = 0;
-    for (int a = threadIdx.x; a < nA; a += TM_NT) {
-        uint32_t lo = (uint32_t)cols[a] * K;
-        if (use_start) {
-            bm_or_field(t.infA, lo, 1, 1u);
-        } else {
-            uint32_t f = bm_field(t.infP1, lo, K);
-            if (f) {
-                bm_or_field(t.infA, lo, K, f);
-                npc++;
-            } else {
-                bm_or_field(t.infA, lo, K, kmask(K));
-            }
-        }
-    }
-    npc = wg_sum(t.sh, npc);
-    STAMP(t, SB_P1);
-    return use_start || (double)npc >= 0.50 * (double)nA;
-}
-
-// collect slots of segments with >= thr synapses onto active cells of
-// `state` by scanning the pool (learning-on form)
-// Scan the segment pool (4 lanes per segment, 16 B of synapse sources each)
-// against the cell bitmap `state`: for every slot, f(slot, meta, eligible,
-// mask of synapses onto cells on in `state`) on all 4 lanes (mask reduced
-// across them).  Only segments with elig(meta) load their rows.  SC_DEPTH
-// batches of 64 segments are in flight per workgroup: meta loads of the
-// batch first, then the row loads, so a pass over the pool costs two HBM
-// round trips per SC_DEPTH x 64 segments.  Returns this thread's bytes.
-#define SC_DEPTH 8
-template <typename E, typename F>
-__device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E elig, F f) {
-    const uint32_t hwm = t.sh->hwm;
-    const uint32_t g = threadIdx.x >> 2, sub = threadIdx.x & 3;
-    uint32_t nb = 0;
-    for (uint32_t base = 0; base < hwm; base += SC_DEPTH * (TM_NT / 4)) {
-        uint32_t m[SC_DEPTH];
-#pragma unroll
-        for (int d = 0; d < SC_DEPTH; d++) {
-            const uint32_t slot = base + d * (TM_NT / 4) + g;
-            m[d] = slot < hwm ? t.meta[slot] : 0u;
-        }
-        uint4 v[SC_DEPTH];
-        bool el[SC_DEPTH];
-#pragma unroll
-        for (int d = 0; d < SC_DEPTH; d++) {
-            const uint32_t slot = base + d * (TM_NT / 4) + g;
-            el[d] = meta_live(m[d]) && elig(m[d]);
-            v[d] = make_uint4(0u, 0u, 0u, 0u);
-            if (el[d] && sub * 8u < meta_nsyn(m[d]))
-                v[d] = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
-        }
-#pragma unroll
-        for (int d = 0; d < SC_DEPTH; d++) {
-            const uint32_t slot = base + d * (TM_NT / 4) + g;
-            if (slot < hwm && sub == 0) nb += 4;
-            const uint32_t nsyn = meta_nsyn(m[d]);
-            uint32_t mask = 0;
-            if (el[d] && sub * 8u < nsyn) {
-                nb += 16;
-                const uint32_t w[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t j = sub * 8 + k;
-                    const uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-                    if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
-                }
-            }
-            mask |= __shfl_xor(mask, 1, 64);
-            mask |= __shfl_xor(mask, 2, 64);
-            f(slot, m[d], el[d], mask);
-        }
-    }
-    return nb;
-}
-
-// collect slots of segments with >= thr synapses onto active cells of
-// `state` by scanning the pool (learning-on form)
-__device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
-    const uint32_t sub = threadIdx.x & 3;
-    uint32_t nb = scan_pool(t, state, [](uint32_t) { return true; },
-                            [&](uint32_t slot, uint32_t, bool el, uint32_t mask) {
-                                if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) {
-                                    const uint32_t i = (uint32_t)atomicAdd(&t.sh->qn, 1);
-                                    if (i < (uint32_t)t.c.q_cap) t.q1[i] = slot;
-                                }
-                            });
-    nb = wg_sum(t.sh, nb);
-    if (threadIdx.x == 0) t.sh->bytes += nb;
-    STAMP(t, SB_SCAN);
-}
-
-// one 16-byte block of a frozen out-list: 8 window-relative u16 ranks,
-// 0xFFFF = padding; bump the rank's u8 counter with non-returning LDS
-// atomics (padding is counted branch-free into a per-lane spare word past
-// the counters, cnt[dummy + lane], so sink updates never collide)
-__device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v, uint32_t dummy) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int h = 0; h < 8; h++) {
-        const uint32_t rel = (w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu;
-        atomicAdd(&cnt[rel != 0xFFFFu ? (rel >> 2) : dummy + (threadIdx.x & 63)], 1u << ((rel & 3) * 8));
-    }
-}
-
-// Stream the 16-byte blocks of lists k < na -- list k is the block range
-// [plo[k], plo[k] + n_k) of ent, pstart the exclusive prefix of n_k with
-// pstart[na] = B -- and count every u16 entry into the u8 counters.  Per
-// pass a block -> list map is built in LDS, then every thread issues its
-// FX_DEPTH block loads before counting any, so one HBM round trip covers
-// FX_OWN blocks whatever the list lengths.
-__device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
-                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy,
-                                          TmSh* shp = nullptr) {
-    for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
-        const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
-        for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
-            const uint32_t a = pstart[k] > lo ? pstart[k] : lo;
-            const uint32_t z = pstart[k + 1] < hi ? pstart[k + 1] : hi;
-            for (uint32_t x = a; x < z; x++) owner[x - lo] = (uint16_t)k;
-        }
-        __syncthreads();
-        STAMP_SH(shp, SB_OWNER);
-        uint4 v[FX_DEPTH];
-#pragma unroll
-        for (int j = 0; j < FX_DEPTH; j++) {
-            const uint32_t x = lo + j * TM_NT + threadIdx.x;
-            v[j] = make_uint4(~0u, ~0u, ~0u, ~0u);
-            if (x < hi) {
-                const uint32_t k = owner[x - lo];
-                v[j] = ent[plo[k] + (x - pstart[k])];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < FX_DEPTH; j++) {
-#ifdef HTM_STAMPS
-            if (j == 0 && threadIdx.x == 0) {
-                __builtin_amdgcn_s_waitcnt(0);  // diagnostic: charge the block loads' latency to SB_SLOAD
-                STAMP_SH(shp, SB_SLOAD);
-            }
-#endif
-            fx_count_block(cnt, v[j], dummy);
-        }
-        STAMP_SH(shp, SB_COUNT);
-        __syncthreads();
-    }
-}
-
-// Every counter byte >= thr (1..127) of cnt[0 .. nbytes), nbytes a multiple
-// of 16: f(index).  Counters never exceed 32, so byte + (128 - thr) sets bit
-// 7 exactly when byte >= thr, without carries between bytes.
-template <typename F>
-__device__ __forceinline__ void fx_qualify(const uint32_t* cnt, uint32_t nbytes, uint32_t thr, F f) {
-    const uint32_t add = 0x01010101u * (128u - thr);
-    const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
-    for (uint32_t i = threadIdx.x; i < nbytes / 16; i += TM_NT) {
-        const uint4 x = c4[i];
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            for (uint32_t m = (w[q] + add) & 0x80808080u; m; m &= m - 1) f(16 * i + 4 * q + ((__ffs(m) - 1) >> 3));
-        }
-    }
-}
-
-// The counter bytes >= thr of the nquads 16-byte quads at cnt, as ranks
-// base + index, appended to dst at sh->qn in ASCENDING order (each thread
-// sweeps a contiguous run of quads; one workgroup scan places the runs), so
-// the qualifying list comes out in rank = (cell, creation) order.  Counters
-// never exceed 32 (see fx_qualify).  Contains barriers: call uniformly.
-// 16-bit hit mask of one counter quad: bit 4j+i set when byte i of word j
-// is >= thr (add = 0x01010101 * (128 - thr); counters never exceed 32)
-__device__ __forceinline__ uint32_t fx_quad_hits(uint4 x, uint32_t add) {
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-    uint32_t h = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t m = (w[j] + add) & 0x80808080u;
-        h |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
-    }
-    return h;
-}
-
-#ifndef FX_CQ
-#define FX_CQ 16  // counter quads one thread sweeps (W <= 16 x 16 x TM_NT bytes)
-#endif
-
-__device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t nquads, uint32_t thr, uint32_t base,
-                                                   TmSh* sh, uint32_t* dst, uint32_t qcap) {
-    const uint32_t add = 0x01010101u * (128u - thr);
-    const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
-    const uint32_t per = (nquads + TM_NT - 1) / TM_NT;  // <= FX_CQ (fx_win <= 64512)
-    const uint32_t q0 = threadIdx.x * per;
-    // one sweep: every quad of the thread's run loaded at once, its hits kept
-    // as 16-bit masks (two per register)
-    uint32_t hm[FX_CQ / 2];
-    uint32_t mine = 0;
-#pragma unroll
-    for (int i = 0; i < FX_CQ; i++) {
-        uint32_t h = 0;
-        if ((uint32_t)i < per && q0 + i < nquads) h = fx_quad_hits(c4[q0 + i], add);
-        if (i & 1) hm[i >> 1] |= h << 16;
-        else hm[i >> 1] = h;
-        mine += __popc(h);
-    }
-    // exclusive prefix over the workgroup in thread order (one barrier)
-    const uint32_t qn0 = (uint32_t)sh->qn;  // thread 0 updates it only after the barrier
-    const uint32_t incl = wave_incl_scan(mine);
-    if (lane_id() == 63) sh->red[TM_NWAVES + wave_id()] = incl;
-    __syncthreads();
-    uint32_t pos = qn0 + incl - mine, tot = 0;
-#pragma unroll
-    for (int v = 0; v < TM_NWAVES; v++) {
-        const uint32_t x = sh->red[TM_NWAVES + v];
-        if (v < (int)wave_id()) pos += x;
-        tot += x;
-    }
-    if (mine) {
-#pragma unroll
-        for (int i = 0; i < FX_CQ; i++) {
-            for (uint32_t m = (hm[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; m; m &= m - 1) {
-                const uint32_t b = __ffs(m) - 1;  // 4 * word + byte
-                if (pos < qcap) dst[pos] = base + 16 * (q0 + i) + b;
-                pos++;
-            }
-        }
-    }
-    if (threadIdx.x == 0) sh->qn = (int32_t)(qn0 + tot);
-}
-
-// zero n 16-byte quads of LDS
-__device__ __forceinline__ void wg_clear4(uint32_t* p, uint32_t nquads) {
-    uint4* p4 = reinterpret_cast<uint4*>(p);
-    for (uint32_t i = threadIdx.x; i < nquads; i += TM_NT) p4[i] = make_uint4(0u, 0u, 0u, 0u);
-}
-
-// learning-off form: forward propagation over the frozen cell->segment index
-// (what Cells4's _outSynapses does).  Pass 0 counts CONNECTED active
-// synapses of the predictive-capable segments (pid lists; counter >=
-// activationThreshold predicts the segment's cell); then, per window of the
-// slot space, all active synapses of every segment (counter >= thr: the
-// segment qualifies for the confidence sum).
-// what collect_frozen counts: the pid pass and every rank window, the pid pass
-// only, or the rank windows only (listing the active cells, or reusing the
-// list a pid-only call left in U)
-enum { FX_ALL = 0, FX_PID = 1, FX_WIN = 2, FX_WIN_REUSE = 3 };
-
-__device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const uint32_t W = (uint32_t)c.fx_win;
-    const uint32_t mac = (uint32_t)c.max_act_cells;
-    uint32_t* cnt = t.U;  // W / 4 counter words + 64 spare (padding sinks)
-    const uint32_t dummy = W / 4;
-    uint16_t* cells = reinterpret_cast<uint16_t*>(t.U + W / 4 + 64);
-    uint32_t* pstart = t.U + W / 4 + 64 + (mac + 1) / 2;
-    uint32_t* plo = pstart + mac + 1;
-    uint16_t* owner = reinterpret_cast<uint16_t*>(plo + mac);
-    uint32_t na;
-    if (mode == FX_WIN_REUSE) {
-        na = (uint32_t)sh->fx_na;
-    } else if (sh->p1_n >= 0 && sh->p1_n <= 64) {
-        // infA is phase 1's: each active column's cells (ascending columns,
-        // ascending cells = the bitmap's order), listed by wave 0, one lane per column
-        if (wave_id() == 0) {
-            const int a = lane_id();
-            const int K = c.K;
-            const int p1n = sh->p1_n;
-            const uint16_t* p1c = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(sh) + sh->p1_off);
-            const uint32_t col = a < p1n ? p1c[a] : 0u;
-            const uint32_t f = a < p1n ? bm_field(t.infA, col * (uint32_t)K, (uint32_t)K) : 0u;
-            const uint32_t n1 = (uint32_t)__popc(f);
-            const uint32_t incl = wave_incl_scan(n1);
-            uint32_t pos = incl - n1;
-            for (uint32_t x = f; x; x &= x - 1) {
-                if (pos < mac) cells[pos] = (uint16_t)(col * (uint32_t)K + (uint32_t)(__ffs(x) - 1));
-                pos++;
-            }
-            const uint32_t tot = __shfl(incl, 63, 64);
-            if (a == 0) sh->fx_na = (int32_t)(tot < mac ? tot : mac);
-        }
-        __syncthreads();
-        na = (uint32_t)sh->fx_na;
-    } else {
-        const uint32_t nact = wg_bitmap_list(t, t.infA, nullptr, cells, mac);
-        na = nact < mac ? nact : mac;
-        if (threadIdx.x == 0) sh->fx_na = (int32_t)na;
-    }
-    const uint32_t nr = t.nr;
-    STAMP(t, SB_LIST);
-    COUNT(t, SC_NACT, na);
-    const uint32_t nwin = (uint32_t)c.fx_nwin;
-    const uint32_t nw = (nr + W - 1) / W;
-    const bool pid_ok = t.np <= (uint32_t)c.fx_pcap;
-    const uint32_t per = (na + TM_NT - 1) / TM_NT;  // <= FX_MAXPER (na <= 64 x 32)
-    const uint32_t k0 = threadIdx.x * per;
-    uint32_t nblk = 0;
-    // block ranges of this thread's cells in pass w: the first FX_PF of them
-    // loaded one pass ahead (registers), any further ones (more than
-    // FX_PF x TM_NT active cells: K > 12) loaded in the pass
-    constexpr uint32_t FX_PF = 2;
-    uint32_t olo[FX_PF], ohi[FX_PF];
-    auto off_idx = [&](int w, uint32_t k) {
-        return w < 0 ? (size_t)c.ncells * nwin + cells[k] : (size_t)cells[k] * nwin + (uint32_t)w;
-    };
-    auto load_offsets = [&](int w) {
-#pragma unroll
-        for (uint32_t j = 0; j < FX_PF; j++) {
-            const uint32_t k = k0 + j;
-            if (j < per && k < na) {
-                const size_t idx = off_idx(w, k);
-                olo[j] = t.fxoff[idx];
-                ohi[j] = t.fxoff[idx + 1];
-            }
-        }
-    };
-    const int w_first = (pid_ok && t.np > 0 && mode != FX_WIN && mode != FX_WIN_REUSE) ? -1 : 0;
-    const int w_end = mode == FX_PID ? 0 : (int)nw;
-    if (w_first < w_end) load_offsets(w_first);
-    for (int w = w_first; w < w_end; w++) {
-        // list of (active cell k, pass w): block range [fxoff[idx], fxoff[idx + 1])
-        uint32_t lsum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < FX_PF; j++) {
-            const uint32_t k = k0 + j;
-            if (j < per && k < na) {
-                plo[k] = olo[j];
-                pstart[k] = ohi[j] - olo[j];
-                lsum += ohi[j] - olo[j];
-            }
-        }
-        for (uint32_t j = FX_PF; j < per; j++) {
-            const uint32_t k = k0 + j;
-            if (k >= na) break;
-            const size_t idx = off_idx(w, k);
-            const uint32_t lo = t.fxoff[idx], hi = t.fxoff[idx + 1];
-            plo[k] = lo;
-            pstart[k] = hi - lo;
-            lsum += hi - lo;
-        }
-        if (w + 1 < w_end) load_offsets(w + 1);
-        uint32_t B;
-        uint32_t pos = wg_excl_scan1(sh, lsum, &B);
-        for (uint32_t j = 0; j < per; j++) {
-            const uint32_t k = k0 + j;
-            if (k >= na) break;
-            const uint32_t n = pstart[k];
-            pstart[k] = pos;
-            pos += n;
-        }
-        if (threadIdx.x == 0) pstart[na] = B;
-        nblk += B;
-        // counters cover the pids (pass -1) or this window's ranks
-        const uint32_t span = w < 0 ? t.np : (nr - (uint32_t)w * W < W ? nr - (uint32_t)w * W : W);
-        const uint32_t nbytes = (span + 15u) & ~15u;
-        wg_clear4(cnt, nbytes / 16);
-        __syncthreads();
-        STAMP(t, SB_WINPRE);
-        COUNT(t, SC_WIN, 1);
-        COUNT(t, SC_BLK, B);
-        fx_stream(t.fxent, plo, pstart, na, B, cnt, owner, dummy, sh);
-        STAMP(t, SB_STREAM);
-        if (w >= 0) fx_collect_ordered(cnt, nbytes / 16, (uint32_t)thr, (uint32_t)w * W, sh, t.q1, (uint32_t)c.q_cap);
-        if (w < 0) {
-            // pid counter >= activationThreshold: the segment's cell is predicted
-            const uint32_t np = t.np;
-            uint32_t* infP = t.infP;
-            const uint16_t* pcell = t.fxpcell;
-            fx_qualify(cnt, nbytes, (uint32_t)c.act_thr, [&](uint32_t pid) {
-                if (pid < np) {
-                    const uint32_t cell = pcell[pid];
-                    atomicOr(&infP[cell >> 5], 1u << (cell & 31));
-                }
-            });
-            __syncthreads();
-        }
-        STAMP(t, SB_QSCAN);
-    }
-    // out-list blocks + the two block offsets of every (active cell, pass)
-    if (threadIdx.x == 0 && w_end > w_first) sh->bytes += 16ull * nblk + 8ull * na * (uint32_t)(w_end - w_first);
-}
-
-// Pass 1 of _inferPhase2 over the qn qualifying segments in t.q1: the
-// predicted cells (rows path; the frozen pid path predicted them while
-// counting), the dutyCycle() each contributes, emit(k, slot, cell, dc).
-// Returns this thread's algorithmic bytes.
-// connected synapses of pool slot `slot` onto active cells (>= activationThreshold
-// predicts the segment's cell); adds the bytes read to nb
-__device__ __forceinline__ uint32_t seg_connected_activity(Tm& t, uint32_t slot, uint32_t nsyn, uint32_t& nb) {
-    nb += 4u + 16u * ((nsyn + 7u) / 8u);
-    const uint32_t cm = t.conn[slot];
-    const uint4* row = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
-    uint32_t n = 0;
-    for (int q = 0; q < 4; q++) {
-        if ((uint32_t)q * 8 >= nsyn) break;
-        uint4 v = row[q];
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k2 = 0; k2 < 8; k2++) {
-            uint32_t j = q * 8 + k2;
-            uint32_t sid = (w[k2 >> 1] >> ((k2 & 1) * 16)) & 0xFFFFu;
-            if (j < nsyn && ((cm >> j) & 1u) && bm_get(t.infA, sid)) n++;
-        }
-    }
-    return n;
-}
-
-template <bool FROZEN, typename F>
-__device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    uint32_t nb = 0;
-    // frozen: the cells the pid counters did not predict (more pids than
-    // fx_pcap) come from the segments' synapse rows
-    const bool rows = FROZEN && t.np > (uint32_t)c.fx_pcap;
-    for (uint32_t k = threadIdx.x; k < qn && FROZEN; k += TM_NT) {
-        // frozen index: cell and the (frozen-iteration) dutyCycle of the
-        // segment of rank q1[k].  The dutyCycle() state update is a store of
-        // the value it returns; the value read never comes from the pool's
-        // record, which streams sharing a model (fleet) may be refreshing.
-        const uint32_t rank = t.q1[k];
-        const uint2 rec = t.fxrec[rank];
-        const uint32_t cell = rec.x & 0xFFFFu;
-        // the dutyCycle() state write stores the same value every time while
-        // the iteration counter is frozen: only the first one after the index
-        // build changes the record (FX_FRESH marks it done, or never needed)
-        uint32_t slot = ~0u;
-        if (!(rec.x & FX_FRESH) || rows) {
-            slot = t.fxrslot[rank];
-            nb += 4u;
-        }
-        if (!(rec.x & FX_FRESH)) {
-            t.duty[(size_t)slot * 3 + 1] = rec.y;
-            t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
-            atomicOr(const_cast<uint32_t*>(&t.fxrec[rank].x), FX_FRESH);
-            nb += 8u;
-        }
-        nb += 8u;
-        if (rows) {
-            const uint32_t nsyn = meta_nsyn(t.meta[slot]);
-            if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
-                atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
-            nb += 4u;
-        }
-        emit(k, rank, cell, __uint_as_float(rec.y));
-    }
-    for (uint32_t k = threadIdx.x; k < qn && !FROZEN; k += TM_NT) {
-        // learning scan: pool slots
-        const uint32_t slot = t.q1[k];
-        const uint32_t m = t.meta[slot];
-        const uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
-        // meta + conn + used source rows + duty-cycle record read and written
-        nb += 4u + 12u + 8u;
-        if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
-            atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
-        emit(k, slot, cell, seg_dc_update(t.duty, slot, sh->lrn_iter, false));
-    }
-    return nb;
-}
-
-// numPredictedCols: columns with a predicted cell (uniform; has barriers)
-__device__ __forceinline__ uint32_t count_predicted_cols(Tm& t) {
-    const DevCfg& c = t.c;
-    uint32_t n = 0;
-    for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
-        if (bm_field(t.infP, (uint32_t)col * c.K, c.K)) n++;
-    return wg_sum(t.sh, n);
-}
-
-// Tail of _inferPhase2 for qn <= q_lds (<= 1024) qualifying segments: the
-// keys col:12 | cellInColumn:5 | slot:27 | k:10 are bitonic-sorted in LDS,
-// each column's confidence is summed over its run in that order -- NuPIC's
-// (column, cell, segment) order -- and the normaliser is folded over the
-// columns in ascending order, so the float32 results are bit-identical to
-// the oracle.  Returns numPredictedCols.
-template <bool FROZEN>
-__device__ __forceinline__ uint32_t phase2_finish_sorted(Tm& t, uint32_t qn) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const int K = c.K;
-    const uint32_t ql = (uint32_t)c.q_lds;
-    uint64_t* qk = reinterpret_cast<uint64_t*>(t.U);     // [ql] keys, sorted in place
-    float* qd = reinterpret_cast<float*>(t.U + 2 * ql);  // [ql] dutyCycle by pass-1 index k
-    float* rs = reinterpret_cast<float*>(t.U + 3 * ql);  // [ql] run sums at run heads, -1 elsewhere
-    uint32_t nb = phase2_pass1<FROZEN>(t, qn, [&](uint32_t k, uint32_t slot, uint32_t cell, float dc) {
-        const uint32_t col = col_of(c, cell);
-        qk[k] = ((uint64_t)col << 42) | ((uint64_t)(cell - col * K) << 37) | ((uint64_t)slot << 10) | k;
-        qd[k] = dc;
-    });
-    uint32_t n2 = 1;  // pad to a power of two with +inf keys
-    while (n2 < qn) n2 <<= 1;
-    for (uint32_t k = qn + threadIdx.x; k < n2; k += TM_NT) qk[k] = ~0ull;
-    nb = wg_sum(sh, nb);
-    if (threadIdx.x == 0) sh->bytes += nb;
-    STAMP(t, SB_FIN1);
-    COUNT(t, SC_QN, qn);
-    COUNT(t, SC_P2, 1);
-    for (uint32_t size = 2; size <= n2; size <<= 1) {
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            for (uint32_t i = threadIdx.x; i < n2 / 2; i += TM_NT) {
-                const uint32_t lo = 2 * i - (i & (stride - 1));
-                const uint32_t hi = lo + stride;
-                const uint64_t a = qk[lo], b = qk[hi];
-                if ((a > b) == ((lo & size) == 0)) {
-                    qk[lo] = b;
-                    qk[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    STAMP(t, SB_SORT);
-    // run heads sum their column in order; -1 marks the other entries
-    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
-        const uint32_t col = (uint32_t)(qk[k] >> 42);
-        if (k > 0 && (uint32_t)(qk[k - 1] >> 42) == col) {
-            rs[k] = -1.0f;
-            continue;
-        }
-        float sum = 0.0f;
-        for (uint32_t j = k; j < qn && (uint32_t)(qk[j] >> 42) == col; j++) sum += qd[qk[j] & 1023u];
-        t.colconf[col] = sum;
-        rs[k] = sum;
-    }
-    __syncthreads();
-    STAMP(t, SB_SUMS);
-    // normaliser: sequential sum over the nonzero columns, ascending (the
-    // -1 markers of non-head entries add +0.0f, which leaves the sum exact)
-    if (threadIdx.x == 0) {
-        float tot = 0.0f;
-#pragma unroll 8
-        for (uint32_t k = 0; k < qn; k++) tot += fmaxf(rs[k], 0.0f);
-        sh->tf[0] = tot;
-    }
-    __syncthreads();
-    const float tot = sh->tf[0];
-    if (tot > 0.0f)
-        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT)
-            if (rs[k] >= 0.0f) t.colconf[(uint32_t)(qk[k] >> 42)] = rs[k] / tot;
-    const uint32_t npcol = count_predicted_cols(t);
-    STAMP(t, SB_FIN2);
-    return npcol;
-}
-
-// Tail of the frozen _inferPhase2: the qualifying segments arrive in rank =
-// (column, cell, creation) order -- NuPIC's summation order -- so each
-// column's confidence is the in-order float sum over its run of the list and
-// the normaliser folds the run sums in ascending column order: bit-identical
-// to the oracle without sorting.  Column and dutyCycle of entry k live in
-// LDS (qn <= q_lds) or, past that, in the HBM scratch (q1 / q2).  Returns
-// numPredictedCols.
-__device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const uint32_t qn = (uint32_t)sh->qn;
-    const uint32_t ql = (uint32_t)c.q_lds;
-    const bool in_lds = qn <= ql;
-    uint16_t* lcol = reinterpret_cast<uint16_t*>(t.U);  // [ql]
-    float* ldc = reinterpret_cast<float*>(t.U + (ql + 1) / 2);  // [ql]
-    uint32_t* gcol = t.q1;
-    float* gdc = reinterpret_cast<float*>(t.q2);
-    uint32_t nb = phase2_pass1<true>(t, qn, [&](uint32_t k, uint32_t, uint32_t cell, float dc) {
-        const uint32_t col = col_of(c, cell);
-        if (in_lds) {
-            lcol[k] = (uint16_t)col;
-            ldc[k] = dc;
-        } else {  // q1[k] (the rank) has been read: reuse the entry
-            gcol[k] = col;
-            gdc[k] = dc;
-        }
-    });
-    nb = wg_sum(sh, nb);  // (barriers)
-    if (threadIdx.x == 0) sh->bytes += nb;
-    STAMP(t, SB_FIN1);
-    COUNT(t, SC_QN, qn);
-    COUNT(t, SC_P2, 1);
-    auto col_at = [&](uint32_t k) -> uint32_t { return in_lds ? (uint32_t)lcol[k] : gcol[k]; };
-    auto dc_at = [&](uint32_t k) -> float { return in_lds ? ldc[k] : gdc[k]; };
-    // run heads sum their column in list order
-    for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
-        const uint32_t col = col_at(k);
-        if (k > 0 && col_at(k - 1) == col) continue;
-        float sum = 0.0f;
-        for (uint32_t j = k; j < qn && col_at(j) == col; j++) sum += dc_at(j);
-        t.colconf[col] = sum;
-    }
-    __syncthreads();
-    STAMP(t, SB_SUMS);
-    // normaliser: sequential over the columns with a qualifying segment,
-    // ascending (= run-head order); wave 0 loads 64 entries at a time and
-    // folds them lane by lane, non-heads adding +0.0f (the sum is unchanged)
-    if (wave_id() == 0) {
-        float tot = 0.0f;
-        for (uint32_t base = 0; base < qn; base += 64) {
-            const uint32_t i = base + lane_id();
-            float v = 0.0f;
-            if (i < qn) {
-                const uint32_t col = col_at(i);
-                if (i == 0 || col_at(i - 1) != col) v = t.colconf[col];
-            }
-            const int vi = __float_as_int(v);
-#pragma unroll
-            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
-        }
-        if (lane_id() == 0) sh->tf[0] = tot;
-    }
-    __syncthreads();
-    const float tot = sh->tf[0];
-    if (tot > 0.0f)
-        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
-            const uint32_t col = col_at(k);
-            if (k == 0 || col_at(k - 1) != col) t.colconf[col] /= tot;
-        }
-    // numPredictedCols: counted by infer_phase2 before the tail when the pid
-    // counters predicted the cells; from the rows read in pass 1 otherwise
-    const uint32_t npcol = t.np > (uint32_t)c.fx_pcap ? count_predicted_cols(t) : (uint32_t)sh->npc_known;
-    STAMP(t, SB_FIN2);
-    return npcol;
-}
-
-// Shared tail of _inferPhase2: predicted cells, duty cycles, confidences in
-// NuPIC order, normalisation.  Returns numPredictedCols (uniform).
-template <bool FROZEN>
-__device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
-    if (FROZEN) return phase2_finish_ranked(t);
-    if (t.c.fin_mode == 1 && (uint32_t)t.sh->qn <= (uint32_t)t.c.q_lds)
-        return phase2_finish_sorted<FROZEN>(t, (uint32_t)t.sh->qn);
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const int K = c.K;
-    const uint32_t qn = (uint32_t)sh->qn;
-    uint32_t* colcnt = t.U;
-    uint16_t* nzcol = reinterpret_cast<uint16_t*>(t.U + c.ncol);
-    uint32_t* nzstart = t.U + c.ncol + (c.ncol + 1) / 2;
-    // qualifying segments (<= q_lds of them): key, dutyCycle, column; and
-    // the same sorted by column bucket
-    const uint32_t ql = (uint32_t)c.q_lds;
-    uint32_t* qkey = nzstart + c.ncol + 1;
-    float* qdc = reinterpret_cast<float*>(qkey + ql);
-    uint32_t* skey = qkey + 2 * ql;
-    float* sdc = reinterpret_cast<float*>(qkey + 3 * ql);
-    uint16_t* qcol = reinterpret_cast<uint16_t*>(qkey + 4 * ql);
-    uint32_t* colbits = qkey + 4 * ql + (ql + 1) / 2;  // [nw] nonzero columns (fin_mode 2)
-    const bool in_lds = qn <= ql;
-    const bool bitmap = c.fin_mode == 2;
-    wg_clear(colcnt, c.ncol);
-    if (bitmap) wg_clear(colbits, c.nw);
-    __syncthreads();
-    STAMP(t, SB_FCLR);
-    // pass 1: connected activity -> predicted; dutyCycle(); bucket counts
-    uint32_t nb = phase2_pass1<FROZEN>(t, qn, [&](uint32_t k, uint32_t slot, uint32_t cell, float dc) {
-        const uint32_t col = col_of(c, cell);
-        atomicAdd(&colcnt[col], 1u);
-        if (bitmap) atomicOr(&colbits[col >> 5], 1u << (col & 31));
-        if (in_lds) {
-            qkey[k] = ((cell - col * K) << 27) | slot;
-            qdc[k] = dc;
-            qcol[k] = (uint16_t)col;
-        }
-    });
-    nb = wg_sum(sh, nb);
-    if (threadIdx.x == 0) sh->bytes += nb;
-    STAMP(t, SB_FIN1);
-    COUNT(t, SC_QN, qn);
-    COUNT(t, SC_P2, 1);
-    // exclusive scan of bucket counts + nonzero column list (ascending)
-    uint32_t tsum, tnz;
-    if (bitmap) {
-        // wave 0 walks the nonzero-column bitmap (lane l: words l, l + 64)
-        if (wave_id() == 0) {
-            const uint32_t l = lane_id();
-            uint32_t zbase = 0, obase = 0;
-            for (int r = 0; r < 2; r++) {
-                const uint32_t wi = l + 64u * r;
-                const uint32_t bits = wi < (uint32_t)c.nw ? colbits[wi] : 0u;
-                uint32_t s = 0;
-                for (uint32_t x = bits; x; x &= x - 1) s += colcnt[wi * 32 + __ffs(x) - 1];
-                const uint32_t nz = __popc(bits);
-                const uint32_t iz = wave_incl_scan(nz), is = wave_incl_scan(s);
-                uint32_t zo = zbase + iz - nz, off = obase + is - s;
-                for (uint32_t x = bits; x; x &= x - 1) {
-                    const uint32_t col = wi * 32 + __ffs(x) - 1;
-                    const uint32_t n = colcnt[col];
-                    nzcol[zo] = (uint16_t)col;
-                    nzstart[zo] = off;
-                    colcnt[col] = off;
-                    zo++;
-                    off += n;
-                }
-                zbase += __shfl(iz, 63, 64);
-                obase += __shfl(is, 63, 64);
-            }
-            if (l == 0) {
-                nzstart[zbase] = obase;
-                sh->ti[2] = (int32_t)zbase;
-                sh->ti[3] = (int32_t)obase;
-            }
-        }
-        __syncthreads();
-        STAMP(t, SB_SORT);
-        tnz = (uint32_t)sh->ti[2];
-        tsum = (uint32_t)sh->ti[3];
-    } else {
-        const int per = (c.ncol + TM_NT - 1) / TM_NT;
-        const int c0 = threadIdx.x * per;
-        uint32_t lsum = 0, lnz = 0;
-        for (int k = 0; k < per; k++) {
-            int col = c0 + k;
-            if (col < c.ncol && colcnt[col]) { lsum += colcnt[col]; lnz++; }
-        }
-        uint32_t off = wg_excl_scan(sh, lsum, &tsum);
-        uint32_t zo = wg_excl_scan(sh, lnz, &tnz);
-        for (int k = 0; k < per; k++) {
-            int col = c0 + k;
-            if (col >= c.ncol) break;
-            uint32_t n = colcnt[col];
-            if (n) {
-                nzcol[zo] = (uint16_t)col;
-                nzstart[zo] = off;
-                zo++;
-            }
-            colcnt[col] = off;
-            off += n;
-        }
-        if (threadIdx.x == 0) nzstart[tnz] = tsum;
-        __syncthreads();
-    }
-    (void)tsum;
-    // pass 2: scatter keys (cellInColumn << 27 | slot) into column buckets
-    if (in_lds) {
-        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
-            const uint32_t pos = atomicAdd(&colcnt[qcol[k]], 1u);
-            skey[pos] = qkey[k];
-            sdc[pos] = qdc[k];
-        }
-    } else {
-        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
-            uint32_t slot = t.q1[k];
-            uint32_t cell = meta_cell(t.meta[slot]);
-            uint32_t col = col_of(c, cell);
-            uint32_t pos = atomicAdd(&colcnt[col], 1u);
-            t.q2[pos] = ((cell - col * K) << 27) | slot;
-        }
-    }
-    __syncthreads();
-    // pass 3a (LDS path): each entry's rank inside its column bucket (keys are
-    // unique: they hold the slot) places its dutyCycle in (cell, slot) order
-    // into qdc, dead since the scatter.  Entry-parallel with independent loads:
-    // a bucket of m entries costs m loads per entry instead of an O(m^2)
-    // dependent insertion sort on one thread.
-    if (in_lds) {
-        for (uint32_t p = threadIdx.x; p < qn; p += TM_NT) {
-            uint32_t lo = 0, hi = tnz;  // last z with nzstart[z] <= p
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (nzstart[mid] <= p) lo = mid;
-                else hi = mid;
-            }
-            const uint32_t b0 = nzstart[lo], b1 = nzstart[lo + 1];
-            const uint32_t key = skey[p];
-            uint32_t r = 0;
-            for (uint32_t j = b0; j < b1; j++) r += skey[j] < key ? 1u : 0u;
-            qdc[b0 + r] = sdc[p];
-        }
-        __syncthreads();
-    }
-    // pass 3: per column, (cell, slot) order; float sum in that order
-    uint32_t npcol = 0;
-    for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) {
-        uint32_t col = nzcol[k], lo = nzstart[k], hi = nzstart[k + 1];
-        float sum = 0.0f;
-        if (in_lds) {
-            for (uint32_t i = lo; i < hi; i++) sum += qdc[i];
-        } else {
-            for (uint32_t i = lo + 1; i < hi; i++) {
-                uint32_t key = t.q2[i];
-                uint32_t j = i;
-                while (j > lo && t.q2[j - 1] > key) { t.q2[j] = t.q2[j - 1]; j--; }
-                t.q2[j] = key;
-            }
-            for (uint32_t i = lo; i < hi; i++) {
-                uint32_t slot = t.q2[i] & 0x7FFFFFFu;
-                sum += __uint_as_float(t.duty[(size_t)slot * 3 + 1]);
-            }
-        }
-        t.colconf[col] = sum;
-        if (bm_field(t.infP, col * K, K)) npcol++;
-    }
-    npcol = wg_sum(sh, npcol);
-    STAMP(t, SB_SUMS);
-    // total in nonzero-column order (ascending), sequentially as NuPIC sums it:
-    // wave 0 loads 64 column sums at a time and folds them lane by lane
-    // (zero padding adds +0.0f, which leaves the sum unchanged)
-    if (wave_id() == 0) {
-        float tot = 0.0f;
-        for (uint32_t base = 0; base < tnz; base += 64) {
-            const uint32_t i = base + lane_id();
-            const float v = i < tnz ? t.colconf[nzcol[i]] : 0.0f;
-            const int vi = __float_as_int(v);
-#pragma unroll
-            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
-        }
-        if (lane_id() == 0) sh->tf[0] = tot;
-    }
-    __syncthreads();
-    float tot = sh->tf[0];
-    if (tot > 0.0f)
-        for (uint32_t k = threadIdx.x; k < tnz; k += TM_NT) t.colconf[nzcol[k]] /= tot;
-    __syncthreads();
-    STAMP(t, SB_FIN2);
-    COUNT(t, SC_TNZ, tnz);
-    return npcol;
-}
-
-// The confidences a frozen phase 2 computes matter only if its state is the
-// one the step keeps: P2_DISCARD -- a backtrack replay before the current
-// pattern (its phase 1 reads only the predicted cells); P2_IF_IN_SEQ -- the
-// step's own phase 2 or a replay's last one (kept exactly when in sequence,
-// otherwise a backtrack or the next start recomputes); P2_KEEP -- always.
-// Skipped confidence sums leave colConfidence zero.  The segments' dutyCycle()
-// state updates happen in every case, as in NuPIC.
-enum { P2_DISCARD = 0, P2_IF_IN_SEQ = 1, P2_KEEP = 2 };
-
-// frozen phase 2 whose confidences are discarded: the dutyCycle() state
-// updates of the qualifying segments only
-__device__ __forceinline__ void phase2_duty_only(Tm& t) {
-    const uint32_t qn = (uint32_t)t.sh->qn;
-    const uint32_t nb = phase2_pass1<true>(t, qn, [](uint32_t, uint32_t, uint32_t, float) {});
-    if (nb) atomicAdd(&t.sh->bytes, (unsigned long long)nb);
-    COUNT(t, SC_QN, qn);
-    COUNT(t, SC_P2, 1);
-}
-
-// murmur3's finaliser: the per-cell term of an active set's hash
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x85ebca6bu;
-    h ^= h >> 13;
-    h *= 0xc2b2ae35u;
-    h ^= h >> 16;
-    return h;
-}
-
-// Log the active cells of a frozen phase 2 whose confidences are discarded
-// (the list a pid-only collection left in U) for tm_fx_flush_kernel, which
-// makes its qualifying segments' dutyCycle() record writes.  The log is a
-// ring of fx_dcap entries per stream; an active set equal to one still in the
-// ring (flushed or not: backtrack replays recur from step to step) is not
-// logged again -- its writes are made or pending.  False when the ring holds
-// fx_dcap unflushed entries: the caller then counts the rank windows itself.
-// Contains barriers: call uniformly.
-__device__ __forceinline__ bool defer_phase2(Tm& t) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const TmBufs& b = *t.tb;
-    const uint32_t dcap = (uint32_t)c.fx_dcap;
-    const uint32_t na = (uint32_t)sh->fx_na;
-    const uint32_t mac = (uint32_t)c.max_act_cells;
-    const uint16_t* cells = reinterpret_cast<const uint16_t*>(t.U + c.fx_win / 4 + 64);
-    const size_t s = (size_t)t.s;
-    // order-independent hash of the set
-    uint32_t h = 0;
-    for (uint32_t k = threadIdx.x; k < na; k += TM_NT) h += fmix32(cells[k] + 0x9e3779b9u);
-    if (threadIdx.x == 0) {  // (the counters are written by thread 0 only)
-        sh->fx_n = b.fx_dn[s];
-        sh->fx_f = b.fx_dflushed[s];
-    }
-    h = fmix32(wg_sum(sh, h) ^ na);
-    const uint32_t n = sh->fx_n, f = sh->fx_f;
-    // the resident entries whose hash and length match: the newest one is compared in full
-    const uint32_t resident = n < dcap ? n : dcap;
-    uint32_t cand = 0xFFFFFFFFu;
-    for (uint32_t i = threadIdx.x; i < resident; i += TM_NT) {
-        const uint32_t e = n - 1u - i;
-        const size_t slot = s * dcap + e % dcap;
-        if (b.fx_dhash[slot] == h && b.fx_dlen[slot] == na) cand = cand < i ? cand : i;
-    }
-    cand = ~wave_max_u32(~cand);  // wave minimum
-    if (lane_id() == 0) sh->red[wave_id()] = cand;
-    __syncthreads();
-    uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-    for (int w = 0; w < TM_NWAVES; w++) best = sh->red[w] < best ? sh->red[w] : best;
-    __syncthreads();
-    if (best != 0xFFFFFFFFu) {
-        const uint16_t* old = b.fx_dlog + (s * dcap + (n - 1u - best) % dcap) * mac;
-        uint32_t diff = 0;
-        for (uint32_t k = threadIdx.x; k < na; k += TM_NT) diff |= old[k] != cells[k] ? 1u : 0u;
-        if (wg_sum(sh, diff) == 0) {
-            if (threadIdx.x == 0) sh->bytes += 2ull * na + 8ull * resident;
-            return true;  // the same set is logged already
-        }
-    }
-    if (n - f >= dcap) return false;
-    const size_t slot = s * dcap + n % dcap;
-    uint16_t* dst = b.fx_dlog + slot * mac;
-    for (uint32_t k = threadIdx.x; k < na; k += TM_NT) dst[k] = cells[k];
-    if (threadIdx.x == 0) {
-        b.fx_dlen[slot] = (uint16_t)na;
-        b.fx_dhash[slot] = h;
-        b.fx_dn[s] = n + 1u;
-        sh->bytes += 2ull * na + 8ull * resident + 8ull;
-    }
-    __syncthreads();
-    return true;
-}
-
-// _inferPhase2()
-template <bool FROZEN>
-__device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
-    TmSh* sh = t.sh;
-    if (threadIdx.x == 0) {
-        sh->st[0]++;
-        sh->qn = 0;
-        sh->npc_known = -1;
-    }
-    wg_clear(t.infP, t.c.cw);
-    wg_clear(reinterpret_cast<uint32_t*>(t.colconf), t.c.ncol);
-    __syncthreads();
-    if (FROZEN && t.defer && need != P2_KEEP && t.np <= (uint32_t)t.c.fx_pcap) {
-        // the predicted cells first (pid pass): a phase 2 whose confidences the
-        // step discards needs nothing else now -- its segments' one-time
-        // dutyCycle() record writes are logged for tm_fx_flush_kernel
-        collect_frozen(t, t.c.act_thr, FX_PID);
-        __syncthreads();
-        const uint32_t npc = count_predicted_cols(t);
-        const bool inSeq = (double)npc >= 0.5 * sh->avg_dens;
-        const bool keep = need == P2_IF_IN_SEQ && inSeq;
-        if (!keep && defer_phase2(t)) return inSeq;
-        collect_frozen(t, t.c.act_thr, FX_WIN_REUSE);
-        __syncthreads();
-        if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)t.c.q_cap) {
-            sh->err |= 16u;
-            sh->qn = t.c.q_cap;
-        }
-        __syncthreads();
-        if (keep) {
-            if (threadIdx.x == 0) sh->npc_known = (int32_t)npc;
-            __syncthreads();
-            (void)phase2_finish<FROZEN>(t);
-        } else {
-            phase2_duty_only(t);
-        }
-        __syncthreads();
-        return inSeq;
-    }
-    if (FROZEN) collect_frozen(t, t.c.act_thr);
-    else collect_scan(t, t.infA, t.c.act_thr);
-    __syncthreads();
-    if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)t.c.q_cap) {
-        sh->err |= 16u;  // qualifying-segment list overflow (fleet q_capacity): results invalid
-        sh->qn = t.c.q_cap;
-    }
-    __syncthreads();
-    if (FROZEN && t.np <= (uint32_t)t.c.fx_pcap) {
-        // the pid counters have predicted the cells: decide first
-        const uint32_t npc = count_predicted_cols(t);
-        const bool inSeq = (double)npc >= 0.5 * sh->avg_dens;
-        if (need == P2_KEEP || (need == P2_IF_IN_SEQ && inSeq)) {
-            if (threadIdx.x == 0) sh->npc_known = (int32_t)npc;
-            __syncthreads();
-            (void)phase2_finish<FROZEN>(t);
-        } else {
-            phase2_duty_only(t);
-        }
-        __syncthreads();
-        return inSeq;
-    }
-    uint32_t npc = phase2_finish<FROZEN>(t);
-    return (double)npc >= 0.5 * sh->avg_dens;
-}
-
-__device__ __forceinline__ const uint16_t* inf_pat(Tm& t, int k) {
-    return t.sh->inf_pat[(t.sh->inf_head + k) % HTM_MAXPAT];
-}
-__device__ __forceinline__ int inf_len(Tm& t, int k) { return t.sh->inf_len[(t.sh->inf_head + k) % HTM_MAXPAT]; }
-__device__ __forceinline__ const uint16_t* lrn_pat(Tm& t, int k) {
-    return t.lrnpat[(t.sh->lrn_head + k) % HTM_MAXPAT];
-}
-__device__ __forceinline__ int lrn_len(Tm& t, int k) { return t.sh->lrn_len[(t.sh->lrn_head + k) % HTM_MAXPAT]; }
-
-// ---------------------------------------------------------------------------
-// Backtrack assist.  _inferBacktrack tries start offsets oldest first and
-// takes the first whose replay (start cells at that pattern, then phase 1/2
-// through the current one) stays in sequence.  While the TM is frozen each
-// replay is a pure function of the pattern history and the model (the only
-// writes, the segments' dutyCycle cache, store the value every replay
-// computes), so the replays can run concurrently: the owner posts its history,
-// workgroups that finished their own stream take start offsets 1, 2, ..., and
-// the owner walks the offsets in NuPIC's order, running the ones nobody took
-// itself and waiting for the others.  The result (and the work counters, which
-// count exactly the replays the serial loop runs) equals the serial loop's.
-//
-// Hand-offs follow the agent-scope release/acquire recipe of
-// MI355X_MICROARCH.md (every storing wave waits vmcnt(0), barrier, lane-0
-// release fence, vmcnt(0), relaxed flag store; the reader polls relaxed, then
-// one acquire fence before any load of the handed-off bytes).
-
-__device__ __forceinline__ void bt_release_store(unsigned long long* w, unsigned long long v) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ bool bt_try_claim(unsigned long long* w, uint32_t epoch) {
-    const unsigned long long old = atomicMax(w, ((unsigned long long)epoch << 2) | 1ull);
-    return old < ((unsigned long long)epoch << 2);
-}
-
-// replay patterns [start, numPrev) of the history from start cells at `start`
-// (the inner loop of _inferBacktrack); final state in infA / infP / colconf
-template <bool FROZEN>
-__device__ __forceinline__ bool bt_replay(Tm& t, int start, int numPrev) {
-    bool inSeq = false;
-    for (int off = start; off < numPrev; off++) {
-        wg_copy(t.infP1, t.infP, t.c.cw);
-        __syncthreads();
-        inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
-        if (!inSeq) break;
-        inSeq = infer_phase2<FROZEN>(t, off == numPrev - 1 ? P2_IF_IN_SEQ : P2_DISCARD);
-        if (!inSeq) break;
-    }
-    return inSeq;
-}
-
-template <bool FROZEN>
-__device__ __forceinline__ void infer_backtrack_assisted(Tm& t, int numPrev, uint32_t* bkA, uint32_t* bkP) {
-    TmSh* sh = t.sh;
-    const DevCfg& c = t.c;
-    const int cw = c.cw;
-    const int cur = numPrev - 1;
-    const TmBufs& b = *t.tb;
-    const uint32_t ep = t.bt_epoch;
-    const size_t s = (size_t)t.s;
-    const size_t rw = 2 * (size_t)cw + (size_t)c.ncol;
-    uint32_t bad = 0;
-    int candStart = -1;
-    // ---- start offset 0 by the owner, unposted: most backtracks lock on there,
-    // and helpers would only burn the CU time the slow owners need
-    if (bt_replay<FROZEN>(t, 0, numPrev)) {
-        candStart = 0;
-    } else {
-        bad = 1u;
-    }
-    const bool post = candStart < 0 && numPrev > 1;
-    if (post) {
-    // ---- post the job: history oldest first, lengths, lrn_iter, avg density
-    uint16_t* jp = b.bt_pat + s * HTM_MAXPAT * HTM_MAXACT;
-    uint32_t* ji = b.bt_info + s * BT_INFO_WORDS;
-    for (int i = threadIdx.x; i < numPrev * HTM_MAXACT; i += TM_NT) {
-        const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
-        if (a < inf_len(t, k)) jp[i] = inf_pat(t, k)[a];
-    }
-    if (threadIdx.x < numPrev) ji[4 + threadIdx.x] = (uint32_t)inf_len(t, threadIdx.x);
-    if (threadIdx.x == 0) {
-        ji[0] = (uint32_t)numPrev;
-        ji[1] = sh->lrn_iter;
-        const unsigned long long ad = (unsigned long long)__double_as_longlong(sh->avg_dens);
-        ji[2] = (uint32_t)ad;
-        ji[3] = (uint32_t)(ad >> 32);
-        // helpers take offsets 2, 3, ...; the owner goes on with 1
-        __hip_atomic_store(&b.bt_take[s], ((unsigned long long)ep << 16) | 2ull, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    bt_release_store(&b.bt_state[s], ((unsigned long long)ep << 16) | (unsigned long long)numPrev);
-    }
-    // ---- walk the remaining start offsets in NuPIC's order
-    for (int start = 1; post && start < numPrev; start++) {
-        unsigned long long* cl = b.bt_claim + s * HTM_MAXPAT + start;
-        if (threadIdx.x == 0) sh->ti[4] = bt_try_claim(cl, ep) ? 1 : 0;
-        __syncthreads();
-        const bool mine = sh->ti[4] != 0;
-        __syncthreads();
-        bool inSeq;
-        if (mine) {
-            inSeq = bt_replay<FROZEN>(t, start, numPrev);
-            if (threadIdx.x == 0)  // helpers never wait for it: mark it done for them
-                __hip_atomic_store(cl, ((unsigned long long)ep << 2) | (inSeq ? 2ull : 3ull), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (threadIdx.x == 0) {
-                unsigned long long v;
-                for (;;) {
-                    v = __hip_atomic_load(cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((v >> 2) == ep && (v & 3ull) >= 2ull) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                sh->ti[4] = (int)(v & 3ull);
-            }
-            __syncthreads();
-            inSeq = sh->ti[4] == 2;
-            // the helper's replay counts as the serial loop's work
-            const uint32_t* mt = b.bt_meta + (s * HTM_MAXPAT + start) * 4;
-            if (threadIdx.x == 0) {
-                sh->bytes += (unsigned long long)mt[0] | ((unsigned long long)mt[1] << 32);
-                sh->st[0] += mt[2];
-                sh->err |= mt[3];
-            }
-            if (inSeq) {
-                const uint32_t* rs = b.bt_res + (s * HTM_MAXPAT + start) * rw;
-                wg_copy(t.infA, rs, cw);
-                if (threadIdx.x == 0) sh->p1_n = -1;  // (infA is no longer phase 1's)
-                wg_copy(t.infP, rs + cw, cw);
-                wg_copy(reinterpret_cast<uint32_t*>(t.colconf), rs + 2 * cw, c.ncol);
-            }
-            __syncthreads();
-        }
-        if (inSeq) {
-            candStart = start;
-            break;
-        }
-        bad |= 1u << start;
-    }
-    // ---- close the job (helpers stop taking its offsets)
-    if (post && threadIdx.x == 0)
-        __hip_atomic_store(&b.bt_state[s], ((unsigned long long)ep << 16) | BT_CLOSED, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (candStart < 0) {
-        wg_copy(t.infA, bkA, cw);
-        if (threadIdx.x == 0) sh->p1_n = -1;
-        __syncthreads();
-        (void)infer_phase2<FROZEN>(t);
-    }
-    if (threadIdx.x == 0) {
-        int npop = 0;
-        for (int i = 0; i < numPrev; i++) {
-            if (((bad >> i) & 1u) || (candStart >= 0 && i <= candStart)) npop++;
-            else break;
-        }
-        sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
-        sh->n_inf_pat -= npop;
-        // scratch traffic: backup out + in, the posted history
-        sh->bytes += 2ull * 4ull * cw + 4ull * cw + (candStart < 0 ? 4ull * cw : 0ull) +
-                     (post ? 2ull * numPrev * HTM_MAXACT : 0ull);
-    }
-    wg_copy(t.infP1, bkP, cw);
-    __syncthreads();
-    (void)cur;
-}
-
-// _inferBacktrack(activeColumns).  gprevP: infPredictedState(t-1) in HBM
-// when the step's state was loaded from there (first step of a run: the
-// write-back comes only at the end of the step), else null.  The replays
-// overwrite the LDS copy, so that one is the backup; otherwise a scratch
-// copy is kept.  NuPIC's saved candidate state is not copied: the loop stops
-// at the candidate, so the live state already is it; and with no candidate
-// the current pattern's phase 1 is recomputed from infP(t-1) instead of
-// restoring a saved infActiveState (same state, computed the same way).
-template <bool FROZEN>
-__device__ __forceinline__ void infer_backtrack(Tm& t, const uint32_t* gprevP) {
-    TmSh* sh = t.sh;
-    const int cw = t.c.cw;
-    const int numPrev = sh->n_inf_pat;
-    if (numPrev <= 0) return;
-    const int cur = numPrev - 1;
-    if (threadIdx.x == 0) sh->st[1]++;
-    const bool assisted = FROZEN && t.bt_epoch;
-    const uint32_t* bkP = gprevP;
-    if (!bkP || assisted) {
-        wg_copy(t.sbm + cw, t.infP1, cw);
-        bkP = t.sbm + cw;
-    }
-    if (assisted) {
-        uint32_t* bkA = t.sbm;
-        wg_copy(bkA, t.infA, cw);
-        __syncthreads();
-        infer_backtrack_assisted<FROZEN>(t, numPrev, bkA, t.sbm + cw);
-        STAMP(t, SB_BT);
-        return;
-    }
-    __syncthreads();
-    uint32_t bad = 0;
-    bool haveCand = false;
-    int candStart = -1;
-    for (int start = 0; start < numPrev; start++) {
-        if (start == cur && haveCand) break;
-        bool inSeq = false;
-        for (int off = start; off < numPrev; off++) {
-            wg_copy(t.infP1, t.infP, cw);
-            __syncthreads();
-            STAMP(t, SB_BT);
-            inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
-            if (!inSeq) break;
-            inSeq = infer_phase2<FROZEN>(t, off == cur ? P2_IF_IN_SEQ : P2_DISCARD);
-            if (!inSeq) break;
-        }
-        if (!inSeq) {
-            bad |= 1u << start;
-            continue;
-        }
-        haveCand = true;
-        candStart = start;
-        break;
-    }
-    wg_copy(t.infP1, bkP, cw);
-    __syncthreads();
-    if (!haveCand) {
-        (void)infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
-        (void)infer_phase2<FROZEN>(t);
-    }
-    if (threadIdx.x == 0) {
-        int npop = 0;
-        for (int i = 0; i < numPrev; i++) {
-            if (((bad >> i) & 1u) || (haveCand && i <= candStart)) npop++;
-            else break;
-        }
-        sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
-        sh->n_inf_pat -= npop;
-        // infP(t-1) backup: scratch out + in, or one read of the HBM state
-        sh->bytes += (gprevP ? 4ull : 8ull) * cw;
-    }
-    STAMP(t, SB_BT);
-}
-
-// _updateInferenceState(activeColumns)
-template <bool FROZEN>
-__device__ __forceinline__ void update_inference(Tm& t, const uint32_t* gprevP) {
-    TmSh* sh = t.sh;
-    if (threadIdx.x == 0) {
-        if (t.c.max_inf_bt > 0) {
-            if (sh->n_inf_pat > t.c.max_inf_bt) {
-                sh->inf_head = (sh->inf_head + 1) % HTM_MAXPAT;
-                sh->n_inf_pat--;
-            }
-            int slot = (sh->inf_head + sh->n_inf_pat) % HTM_MAXPAT;
-            sh->inf_len[slot] = (uint16_t)sh->nA;
-            sh->ti[0] = slot;
-            sh->n_inf_pat++;
-        } else {
-            sh->ti[0] = -1;
-        }
-    }
-    __syncthreads();
-    if (sh->ti[0] >= 0)
-        for (int a = threadIdx.x; a < sh->nA; a += TM_NT) sh->inf_pat[sh->ti[0]][a] = sh->act[a];
-    __syncthreads();
-    bool inSeq = infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
-    if (!inSeq) {
-        infer_backtrack<FROZEN>(t, gprevP);
-        return;
-    }
-    // with a pattern history, a phase 2 out of sequence is redone by the backtrack
-    inSeq = infer_phase2<FROZEN>(t, sh->n_inf_pat > 0 ? P2_IF_IN_SEQ : P2_KEEP);
-    if (!inSeq) infer_backtrack<FROZEN>(t, gprevP);
-}
-
-// ---------------------------------------------------------------------------
-// Learning (wave-0 sequential helpers run with all 64 lanes of wave 0)
-
-// per-column best (activity, cellInColumn, first segment) key over the pool
-// for segments with >= thr synapses onto `state`; only columns flagged in
-// `colflags` when it is non-null.  _getBestMatchingCell for many columns.
-__device__ __forceinline__ void scan_best(Tm& t, const uint32_t* state, int thr, const uint32_t* colflags) {
-    const DevCfg& c = t.c;
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
-    const uint32_t sub = threadIdx.x & 3;
-    uint32_t nb = scan_pool(
-        t, state,
-        [&](uint32_t m) {
-            const uint32_t col = col_of(c, meta_cell(m));
-            return !colflags || ((colflags[col >> 5] >> (col & 31)) & 1u);
-        },
-        [&](uint32_t slot, uint32_t m, bool el, uint32_t mask) {
-            const uint32_t n = __popc(mask);
-            if (el && sub == 0 && n >= (uint32_t)thr) {
-                const uint32_t cell = meta_cell(m), col = col_of(c, cell);
-                const uint32_t cic = cell - col * c.K;
-                const unsigned long long key = ((unsigned long long)n << 40) | ((unsigned long long)cic << 32) |
-                                               (unsigned long long)(0xFFFFFFFFu - slot);
-                atomicMax(&keys[col], key);
-            }
-        });
-    nb = wg_sum(t.sh, nb);
-    if (threadIdx.x == 0) t.sh->bytes += nb;
-}
-
-__device__ __forceinline__ uint32_t key_slot(unsigned long long k) { return 0xFFFFFFFFu - (uint32_t)k; }
-__device__ __forceinline__ uint32_t key_cic(unsigned long long k) { return (uint32_t)(k >> 32) & 0xFFu; }
-__device__ __forceinline__ uint32_t key_act(unsigned long long k) { return (uint32_t)(k >> 40); }
-
-struct WUpd {
-    uint32_t mask;   // active existing synapse positions
-    uint32_t n_new;  // new sources
-    uint32_t my_new; // lane k (< n_new): k-th new source
-};
-
-// _getSegmentActiveSynapses(c, i, s, activeState, newSynapses) with
-// _chooseCellsToLearnFrom; candidates = sh->cand (cells on in `state`).
-// slot == 0xFFFFFFFF: new segment.
-__device__ __forceinline__ WUpd w_build_update(Tm& t, uint32_t slot, const uint32_t* state, bool want_new) {
-    TmSh* sh = t.sh;
-    const int l = lane_id();
-    const bool exist = slot != 0xFFFFFFFFu;
-    uint32_t nsyn = exist ? meta_nsyn(t.meta[slot]) : 0u;
-    uint32_t mysrc = (exist && (uint32_t)l < nsyn) ? (uint32_t)t.src[(size_t)slot * HTM_MAXSYN + l] : 0xFFFFFFFFu;
-    bool act = (exist && (uint32_t)l < nsyn) && bm_get(state, mysrc);
-    WUpd u;
-    u.mask = (uint32_t)__ballot(act);
-    u.n_new = 0;
-    u.my_new = 0;
-    if (l == 0 && exist) atomicAdd(&sh->bytes, (unsigned long long)(4 + 2 * nsyn));
-    int n = want_new ? t.c.new_syn - __popc(u.mask) : 0;
-    if (n <= 0) return u;
-    const int ncand = sh->ncand;
-    uint32_t cv = l < ncand ? sh->cand[l] : 0xFFFFFFFEu;
-    bool ok = l < ncand;
-    for (uint32_t j = 0; j < nsyn; j++) {
-        uint32_t sj = __shfl(mysrc, (int)j, 64);
-        if (cv == sj) ok = false;
-    }
-    uint64_t keep = __ballot(ok);
-    const uint32_t m = (uint32_t)__popcll(keep);
-    if (m == 0) return u;
-    const uint32_t pos = ballot_rank(keep);
-    uint64_t chosen;
-    if (m <= (uint32_t)n) {
-        chosen = (m == 64) ? ~0ull : ((1ull << m) - 1ull);
-    } else {
-        uint64_t ch = 0;
-        if (l == 0) {
-            int32_t f = sh->rf, r = sh->rr;
-            if (n == 1) {
-                ch = 1ull << rng_u32(sh->rng, f, r, m);
-            } else {
-                uint32_t cnt = 0;
-                for (uint32_t i = 0; i < m; i++) {
-                    if (rng_u32(sh->rng, f, r, m - i) < (uint32_t)n - cnt) {
-                        ch |= 1ull << i;
-                        if (++cnt == (uint32_t)n) break;
-                    }
-                }
-            }
-            sh->rf = f;
-            sh->rr = r;
-        }
-        chosen = __shfl(ch, 0, 64);
-    }
-    if (ok && ((chosen >> pos) & 1ull)) {
-        uint32_t op = (uint32_t)__popcll(chosen & ((1ull << pos) - 1ull));
-        sh->newsrc[op] = cv;
-    }
-    u.n_new = (uint32_t)__popcll(chosen);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    u.my_new = (uint32_t)l < u.n_new ? sh->newsrc[l] : 0u;
-    return u;
-}
-
-__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-    return v;
-}
-
-// _adaptSegment on an existing segment; returns trimSegment (wave-uniform)
-__device__ __forceinline__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t n_new, uint32_t my_new) {
-    const DevCfg& c = t.c;
-    const int l = lane_id();
-    const uint32_t m = t.meta[slot];
-    const uint32_t nsyn = meta_nsyn(m);
-    uint16_t* srow = t.src + (size_t)slot * HTM_MAXSYN;
-    float* prow = t.perm + (size_t)slot * HTM_MAXSYN;
-    if (l == 0) {
-        t.duty[(size_t)slot * 3] += 1u;  // positiveActivations
-        (void)seg_dc_update(t.duty, slot, t.sh->lrn_iter, true);
-        // meta, duty (r/w), sources + permanences (r/w), conn
-        atomicAdd(&t.sh->bytes, (unsigned long long)(4 + 24 + 2 * 6 * (nsyn + n_new) + 8));
-    }
-    const bool in = (uint32_t)l < nsyn;
-    uint32_t sj = in ? srow[l] : 0u;
-    float p = in ? prow[l] : 0.0f;
-    const bool isact = in && ((amask >> l) & 1u);
-    const bool inact = in && !isact;
-    bool hit0 = false;
-    if (inact) {
-        float nv = p + (-c.tm_dec);
-        p = nv;
-        if (nv <= 0.0f) { p = 0.0f; hit0 = true; }
-    }
-    if (isact) {
-        float nv = p + c.tm_inc;
-        p = nv;
-        if (nv > c.tm_max) p = c.tm_max;
-    }
-    const bool trim = __ballot(hit0) != 0ull;
-    bool del = false;
-    if (nsyn + n_new > (uint32_t)c.max_syn) {
-        const uint32_t numToFree = nsyn + n_new - (uint32_t)c.max_syn;
-        uint32_t rin = 0, rac = 0;
-        for (int k = 0; k < 32; k++) {
-            float pk = __shfl(p, k, 64);
-            int ik = __shfl((int)inact, k, 64);
-            int ak = __shfl((int)isact, k, 64);
-            bool lt = (pk < p) || (pk == p && k < l);
-            if (ik && lt) rin++;
-            if (ak && lt) rac++;
-        }
-        const uint32_t ninact = (uint32_t)__popcll(__ballot(inact));
-        if (inact && rin < numToFree) del = true;
-        if (numToFree > ninact && isact && rac < numToFree - ninact) del = true;
-    }
-    const bool keep = in && !del;
-    const uint64_t kb = __ballot(keep);
-    const uint32_t nkeep = (uint32_t)__popcll(kb);
-    const uint32_t np = ballot_rank(kb);
-    uint32_t cbits = 0;
-    if (keep) {
-        srow[np] = (uint16_t)sj;
-        prow[np] = p;
-        if (p >= c.tm_conn) cbits |= 1u << np;
-    }
-    if ((uint32_t)l < n_new) {
-        srow[nkeep + l] = (uint16_t)my_new;
-        prow[nkeep + l] = c.init_perm;
-        if (c.init_perm >= c.tm_conn) cbits |= 1u << (nkeep + l);
-    }
-    cbits = wave_or_u32(cbits);
-    if (l == 0) {
-        t.conn[slot] = cbits;
-        t.meta[slot] = (m & ~(0x3Fu << 16)) | ((nkeep + n_new) << 16);
-    }
-    return trim;
-}
-
-// _trimSegmentsInCell(c, i, [s], minPermanence=0.00001, minNumSyns=0)
-__device__ __forceinline__ void w_trim_segment(Tm& t, uint32_t slot) {
-    const DevCfg& c = t.c;
-    const int l = lane_id();
-    const uint32_t m = t.meta[slot];
-    const uint32_t nsyn = meta_nsyn(m), cell = meta_cell(m);
-    uint16_t* srow = t.src + (size_t)slot * HTM_MAXSYN;
-    float* prow = t.perm + (size_t)slot * HTM_MAXSYN;
-    const bool in = (uint32_t)l < nsyn;
-    uint32_t sj = in ? srow[l] : 0u;
-    float p = in ? prow[l] : 0.0f;
-    const bool del = in && p < 0.00001f;
-    const uint32_t ndel = (uint32_t)__popcll(__ballot(del));
-    if (l == 0) atomicAdd(&t.sh->bytes, (unsigned long long)(4 + 6 * nsyn + (ndel ? 8 + 6 * (nsyn - ndel) : 0)));
-    if (ndel == nsyn) {
-        if (l == 0) {
-            t.meta[slot] = m & ~(1u << 23);
-            t.nseg[cell] -= 1;
-            atomicSub(&t.sh->nlive, 1u);
-        }
-        return;
-    }
-    if (ndel == 0) return;
-    const bool keep = in && !del;
-    const uint64_t kb = __ballot(keep);
-    const uint32_t np = ballot_rank(kb);
-    uint32_t cbits = 0;
-    if (keep) {
-        srow[np] = (uint16_t)sj;
-        prow[np] = p;
-        if (p >= c.tm_conn) cbits |= 1u << np;
-    }
-    cbits = wave_or_u32(cbits);
-    if (l == 0) {
-        t.conn[slot] = cbits;
-        t.meta[slot] = (m & ~(0x3Fu << 16)) | ((nsyn - ndel) << 16);
-    }
-}
-
-// new sequence segment on `cell` with the chosen sources
-__device__ __forceinline__ void w_create_segment(Tm& t, uint32_t cell, uint32_t n_new, uint32_t my_new) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const int l = lane_id();
-    uint32_t slot = sh->hwm;
-    if (slot >= (uint32_t)c.seg_cap) {
-        if (l == 0) sh->err |= 1u;
-        return;
-    }
-    if ((uint32_t)l < n_new) {
-        t.src[(size_t)slot * HTM_MAXSYN + l] = (uint16_t)my_new;
-        t.perm[(size_t)slot * HTM_MAXSYN + l] = c.init_perm;
-    }
-    if (l == 0) {
-        uint32_t cm = 0;
-        if (c.init_perm >= c.tm_conn) cm = n_new >= 32 ? 0xFFFFFFFFu : ((1u << n_new) - 1u);
-        t.conn[slot] = cm;
-        t.meta[slot] = make_meta(cell, n_new, 1u, 1u);
-        uint32_t* d = t.duty + (size_t)slot * 3;
-        d[0] = 1u;
-        d[1] = __float_as_uint((float)(1.0 / (double)sh->lrn_iter));
-        d[2] = sh->lrn_iter;
-        atomicAdd(&sh->bytes, (unsigned long long)(4 + 4 + 12 + 6 * n_new + 1));
-        t.nseg[cell] += 1;
-        sh->hwm = slot + 1;
-        sh->nlive += 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
-// _getCellForNewSegment(colIdx); returns the cell index within the column
-__device__ __forceinline__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const int l = lane_id();
-    const int K = c.K;
-    const int minIdx = K == 1 ? 0 : 1, maxIdx = K == 1 ? 0 : K - 1;
-    bool ok = l >= minIdx && l <= maxIdx && (int)t.nseg[col * K + l] < c.max_segs_per_cell;
-    uint64_t b = __ballot(ok);
-    uint32_t m = (uint32_t)__popcll(b);
-    if (m > 0) {
-        uint32_t idx = 0;
-        if (l == 0) {
-            int32_t f = sh->rf, r = sh->rr;
-            idx = rng_u32(sh->rng, f, r, m);
-            sh->rf = f;
-            sh->rr = r;
-        }
-        idx = __shfl(idx, 0, 64);
-        // position of the idx-th set bit of b
-        uint64_t x = b;
-        for (uint32_t k = 0; k < idx; k++) x &= x - 1ull;
-        return (uint32_t)(__ffsll((unsigned long long)x) - 1);
-    }
-    // all cells full: free the least-used segment of the column
-    unsigned long long best = ~0ull;
-    const uint32_t hwm = sh->hwm;
-    for (uint32_t slot = l; slot < hwm; slot += 64) {
-        uint32_t mm = t.meta[slot];
-        if (!meta_live(mm)) continue;
-        uint32_t cell = meta_cell(mm);
-        if (col_of(c, cell) != col) continue;
-        uint32_t cic = cell - col * K;
-        if ((int)cic < minIdx) continue;
-        float dc = seg_dc_update(t.duty, slot, sh->lrn_iter, false);
-        unsigned long long key = ((unsigned long long)__float_as_uint(dc) << 32) | ((unsigned long long)cic << 27) | slot;
-        best = key < best ? key : best;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long tt = __shfl_xor(best, o, 64);
-        best = tt < best ? tt : best;
-    }
-    if (best == ~0ull || __uint_as_float((uint32_t)(best >> 32)) >= 1.0f) return (uint32_t)minIdx;
-    uint32_t slot = (uint32_t)best & 0x7FFFFFFu;
-    uint32_t cic = (uint32_t)(best >> 27) & 0x1Fu;
-    if (l == 0) {
-        uint32_t mm = t.meta[slot];
-        t.meta[slot] = mm & ~(1u << 23);
-        t.nseg[meta_cell(mm)] -= 1;
-        sh->nlive -= 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    return cic;
-}
-
-// cells on in `bm` -> sh->cand (<= HTM_MAXACT, ascending)
-__device__ __forceinline__ void build_cand(Tm& t, const uint32_t* bm) {
-    uint32_t n = wg_bitmap_list(t, bm, t.sh->cand, nullptr, HTM_MAXACT);
-    if (threadIdx.x == 0) {
-        if (n > HTM_MAXACT) { t.sh->err |= 8u; n = HTM_MAXACT; }
-        t.sh->ncand = (int32_t)n;
-    }
-    __syncthreads();
-}
-
-// _processSegmentUpdates(activeColumns)
-__device__ __forceinline__ void process_segment_updates(Tm& t, const uint16_t* cols, int nA) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    wg_clear(t.flags, c.nw);
-    __syncthreads();
-    for (int a = threadIdx.x; a < nA; a += TM_NT) atomicOr(&t.flags[cols[a] >> 5], 1u << (cols[a] & 31));
-    __syncthreads();
-    const int n = sh->n_upd;
-    uint32_t* tflag = t.U;
-    for (int k = wave_id(); k < n; k += TM_NWAVES) {
-        const htm_tm_update& e = t.upd[k];
-        uint32_t col = e.col;
-        bool doit = ((t.flags[col >> 5] >> (col & 31)) & 1u) && (sh->lrn_iter - e.date <= (uint32_t)c.upd_valid);
-        bool trim = false;
-        if (doit) {
-            uint32_t nn = e.n_new;
-            uint32_t my_new = (uint32_t)lane_id() < nn ? e.new_src[lane_id()] : 0u;
-            trim = w_adapt_existing(t, e.slot, e.active_mask, nn, my_new);
-        }
-        if (lane_id() == 0) tflag[k] = trim ? 1u : 0u;
-    }
-    __syncthreads();
-    for (int k = wave_id(); k < n; k += TM_NWAVES)
-        if (tflag[k]) w_trim_segment(t, t.upd[k].slot);
-    __syncthreads();
-    if (threadIdx.x == 0) sh->n_upd = 0;
-    __syncthreads();
-}
-
-// _learnPhase1(activeColumns, readOnly)
-__device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA, bool ro) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const int K = c.K;
-    wg_clear(t.lrnA, c.cw);
-    wg_clear(t.flags, c.nw);
-    __syncthreads();
-    uint32_t nun = 0;
-    for (int a = threadIdx.x; a < nA; a += TM_NT) {
-        uint32_t col = cols[a];
-        uint32_t f = bm_field(t.lrnP1, col * K, K);
-        int pc = __popc(f);
-        if (pc == 1) {
-            bm_or_field(t.lrnA, col * K, K, f);
-        } else {
-            nun++;
-            atomicOr(&t.flags[col >> 5], 1u << (col & 31));
-            if (pc > 1) atomicOr(&sh->err, 4u);
-        }
-    }
-    nun = wg_sum(sh, nun);
-    const bool inSeq = (int)nun < nA / 2;
-    if (ro || nun == 0) return inSeq;
-    wg_clear(t.U, 2 * c.ncol);
-    __syncthreads();
-    scan_best(t, t.lrnA1, c.min_thr, t.flags);
-    __syncthreads();
-    build_cand(t, t.lrnA1);
-    const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
-    if (wave_id() == 0) {
-        for (int a = 0; a < nA; a++) {
-            uint32_t col = cols[a];
-            if (!((t.flags[col >> 5] >> (col & 31)) & 1u)) continue;
-            unsigned long long key = keys[col];
-            bool seqseg = false;
-            uint32_t slot = 0, cic = 0;
-            if (key) {
-                slot = key_slot(key);
-                cic = key_cic(key);
-                seqseg = meta_seq(t.meta[slot]) != 0u;
-            }
-            if (key && seqseg) {
-                if (lane_id() == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
-                WUpd u = w_build_update(t, slot, t.lrnA1, true);
-                bool trim = w_adapt_existing(t, slot, u.mask, u.n_new, u.my_new);
-                if (trim) w_trim_segment(t, slot);
-            } else {
-                cic = w_cell_for_new_segment(t, col);
-                if (lane_id() == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
-                WUpd u = w_build_update(t, 0xFFFFFFFFu, t.lrnA1, true);
-                w_create_segment(t, col * K + cic, u.n_new, u.my_new);
-            }
-        }
-    }
-    __syncthreads();
-    return inSeq;
-}
-
-// _learnPhase2(readOnly)
-__device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    const int K = c.K;
-    if (threadIdx.x == 0) sh->st[2]++;
-    wg_clear(t.lrnP, c.cw);
-    wg_clear(t.U, 2 * c.ncol);
-    __syncthreads();
-    scan_best(t, t.lrnA, c.act_thr, nullptr);
-    __syncthreads();
-    const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
-    for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
-        unsigned long long key = keys[col];
-        if (key) bm_or_field(t.lrnP, (uint32_t)col * K + key_cic(key), 1, 1u);
-    }
-    __syncthreads();
-    if (ro) return;
-    build_cand(t, t.lrnA);
-    if (wave_id() == 0) {
-        for (int base = 0; base < c.ncol; base += 64) {
-            uint64_t b = __ballot(keys[base + lane_id()] != 0ull);
-            while (b) {
-                int bit = __ffsll((unsigned long long)b) - 1;
-                b &= b - 1ull;
-                uint32_t col = (uint32_t)(base + bit);
-                unsigned long long key = keys[col];
-                uint32_t slot = key_slot(key), act = key_act(key);
-                WUpd u = w_build_update(t, slot, t.lrnA, act < (uint32_t)c.new_syn);
-                if (u.mask == 0u && u.n_new == 0u) continue;
-                int idx = sh->n_upd;
-                if (idx >= c.upd_cap) {
-                    if (lane_id() == 0) sh->err |= 2u;
-                    continue;
-                }
-                htm_tm_update& e = t.upd[idx];
-                if ((uint32_t)lane_id() < u.n_new) e.new_src[lane_id()] = (uint16_t)u.my_new;
-                if (lane_id() == 0) {
-                    e.slot = slot;
-                    e.col = (uint16_t)col;
-                    e.cell = (uint8_t)key_cic(key);
-                    e.n_new = (uint8_t)u.n_new;
-                    e.active_mask = u.mask;
-                    e.date = sh->lrn_iter;
-                    sh->n_upd = idx + 1;
-                    // queued entry written now and read back at the next step
-                    atomicAdd(&sh->bytes, (unsigned long long)(2 * (16 + 2 * u.n_new)));
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-    }
-    __syncthreads();
-}
-
-// start cells (cell 0) of the given columns into lrnA
-__device__ __forceinline__ void set_start_cells(Tm& t, uint32_t* bm, const uint16_t* cols, int nA) {
-    wg_clear(bm, t.c.cw);
-    __syncthreads();
-    for (int a = threadIdx.x; a < nA; a += TM_NT) bm_or_field(bm, (uint32_t)cols[a] * t.c.K, 1, 1u);
-    __syncthreads();
-}
-
-// _learnBacktrackFrom(startOffset, readOnly)
-__device__ __forceinline__ bool learn_backtrack_from(Tm& t, int start, bool ro) {
-    TmSh* sh = t.sh;
-    const int cw = t.c.cw;
-    const int numPrev = sh->n_lrn_pat;
-    const int cur = numPrev - 1;
-    if (!ro) {
-        if (threadIdx.x == 0) sh->n_upd = 0;
-        __syncthreads();
-    }
-    bool inSeq = true;
-    for (int off = start; off < numPrev; off++) {
-        wg_copy(t.lrnP1, t.lrnP, cw);
-        wg_copy(t.lrnA1, t.lrnA, cw);
-        __syncthreads();
-        const uint16_t* pat = lrn_pat(t, off);
-        const int len = lrn_len(t, off);
-        if (!ro) process_segment_updates(t, pat, len);
-        if (off == start) {
-            set_start_cells(t, t.lrnA, pat, len);
-            inSeq = true;
-        } else {
-            inSeq = learn_phase1(t, pat, len, ro);
-        }
-        if (!inSeq || off == cur) break;
-        learn_phase2(t, ro);
-    }
-    return inSeq;
-}
-
-// _learnBacktrack(): steps backtracked, 0 on failure
-__device__ __forceinline__ int learn_backtrack(Tm& t) {
-    TmSh* sh = t.sh;
-    const int numPrev = sh->n_lrn_pat - 1;
-    if (numPrev <= 0) return 0;
-    if (threadIdx.x == 0) sh->st[3]++;
-    uint32_t bad = 0;
-    bool inSeq = false;
-    int start;
-    for (start = 0; start < numPrev; start++) {
-        inSeq = learn_backtrack_from(t, start, true);
-        if (inSeq) break;
-        bad |= 1u << start;
-    }
-    if (!inSeq) {
-        if (threadIdx.x == 0) sh->n_lrn_pat = 0;
-        __syncthreads();
-        return 0;
-    }
-    (void)learn_backtrack_from(t, start, false);
-    if (threadIdx.x == 0) {
-        int npop = 0;
-        for (int i = 0; i < numPrev; i++) {
-            if (((bad >> i) & 1u) || i <= start) npop++;
-            else break;
-        }
-        sh->lrn_head = (sh->lrn_head + npop) % HTM_MAXPAT;
-        sh->n_lrn_pat -= npop;
-    }
-    __syncthreads();
-    return numPrev - start;
-}
-
-// _updateLearningState(activeColumns)
-__device__ __forceinline__ void update_learning(Tm& t) {
-    const DevCfg& c = t.c;
-    TmSh* sh = t.sh;
-    // lrnA1 / lrnP1 hold time t-1 (loaded at entry)
-    if (threadIdx.x == 0) {
-        if (c.max_lrn_bt > 0) {
-            if (sh->n_lrn_pat > c.max_lrn_bt) {
-                sh->lrn_head = (sh->lrn_head + 1) % HTM_MAXPAT;
-                sh->n_lrn_pat--;
-            }
-            int slot = (sh->lrn_head + sh->n_lrn_pat) % HTM_MAXPAT;
-            sh->lrn_len[slot] = (uint16_t)sh->nA;
-            sh->ti[1] = slot;
-            sh->n_lrn_pat++;
-        } else {
-            sh->ti[1] = -1;
-        }
-    }
-    __syncthreads();
-    if (sh->ti[1] >= 0)
-        for (int a = threadIdx.x; a < sh->nA; a += TM_NT) t.lrnpat[sh->ti[1]][a] = sh->act[a];
-    __syncthreads();
-    process_segment_updates(t, sh->act, sh->nA);
-    if (threadIdx.x == 0) {
-        if (sh->pam > 0) sh->pam--;
-        sh->lsl++;
-    }
-    __syncthreads();
-    if (!sh->reset) {
-        bool inSeq = learn_phase1(t, sh->act, sh->nA, false);
-        if (inSeq && threadIdx.x == 0) sh->pam = c.pam_len;
-        __syncthreads();
-    }
-    if (sh->reset || sh->pam == 0 || (c.max_seq_len != 0 && sh->lsl >= c.max_seq_len)) {
-        if (threadIdx.x == 0) {
-            int seqLength = sh->pam == 0 ? sh->lsl - c.pam_len : sh->lsl;
-            double alpha = sh->lrn_iter < 100 ? 0.5 : 0.1;
-            sh->avg_lsl = (1.0 - alpha) * sh->avg_lsl + alpha * (double)seqLength;
-        }
-        __syncthreads();
-        int backSteps = 0;
-        if (!sh->reset) backSteps = learn_backtrack(t);
-        if (sh->reset || backSteps == 0) {
-            backSteps = 0;
-            set_start_cells(t, t.lrnA, sh->act, sh->nA);
-            if (threadIdx.x == 0) sh->n_lrn_pat = 0;
-        }
-        if (threadIdx.x == 0) {
-            sh->pam = c.pam_len;
-            sh->lsl = backSteps;
-            sh->n_upd = 0;
-        }
-        __syncthreads();
-    }
-    learn_phase2(t, false);
-}
-
-// stable compaction of live segments (slot order preserved) so that a
-// learning step always has seg_reserve free slots
-__device__ __forceinline__ void compact_pool(Tm& t) {
-    TmSh* sh = t.sh;
-    const uint32_t hwm = sh->hwm;
-    uint32_t base = 0;
-    // pass 1: new slot of every live segment -> q1
-    for (uint32_t c0 = 0; c0 < hwm; c0 += TM_NT) {
-        uint32_t slot = c0 + threadIdx.x;
-        bool live = slot < hwm && meta_live(t.meta[slot]);
-        uint32_t tot;
-        uint32_t pos = wg_excl_scan(sh, live ? 1u : 0u, &tot);
-        if (slot < hwm) t.q1[slot] = live ? base + pos : 0xFFFFFFFFu;
-        base += tot;
-    }
-    __syncthreads();
-    // pass 2: move in increasing slot order (destinations never exceed sources)
-    for (uint32_t c0 = 0; c0 < hwm; c0 += TM_NT) {
-        uint32_t slot = c0 + threadIdx.x;
-        uint32_t ns = slot < hwm ? t.q1[slot] : 0xFFFFFFFFu;
-        uint32_t mm = 0, cm = 0, d0 = 0, d1 = 0, d2 = 0;
-        uint4 sv[4];
-        float4 pv[8];
-#pragma unroll
-        for (int k = 0; k < 4; k++) sv[k] = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-        for (int k = 0; k < 8; k++) pv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ns != 0xFFFFFFFFu) {
-            mm = t.meta[slot];
-            cm = t.conn[slot];
-            d0 = t.duty[(size_t)slot * 3];
-            d1 = t.duty[(size_t)slot * 3 + 1];
-            d2 = t.duty[(size_t)slot * 3 + 2];
-            const uint4* sr = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
-            const float4* pr = reinterpret_cast<const float4*>(t.perm + (size_t)slot * HTM_MAXSYN);
-#pragma unroll
-            for (int k = 0; k < 4; k++) sv[k] = sr[k];
-#pragma unroll
-            for (int k = 0; k < 8; k++) pv[k] = pr[k];
-        }
-        __syncthreads();
-        if (ns != 0xFFFFFFFFu && ns != slot) {
-            t.meta[ns] = mm;
-            t.conn[ns] = cm;
-            t.duty[(size_t)ns * 3] = d0;
-            t.duty[(size_t)ns * 3 + 1] = d1;
-            t.duty[(size_t)ns * 3 + 2] = d2;
-            uint4* sw = reinterpret_cast<uint4*>(t.src + (size_t)ns * HTM_MAXSYN);
-            float4* pw = reinterpret_cast<float4*>(t.perm + (size_t)ns * HTM_MAXSYN);
-#pragma unroll
-            for (int k = 0; k < 4; k++) sw[k] = sv[k];
-#pragma unroll
-            for (int k = 0; k < 8; k++) pw[k] = pv[k];
-        }
-        __syncthreads();
-    }
-    // queued updates follow their segments
-    for (int k = threadIdx.x; k < sh->n_upd; k += TM_NT) t.upd[k].slot = t.q1[t.upd[k].slot];
-    for (uint32_t slot = base + threadIdx.x; slot < hwm; slot += TM_NT) t.meta[slot] = 0u;
-    __syncthreads();
-    if (threadIdx.x == 0) sh->hwm = base;
-    __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// One BacktrackingTM.compute + raw anomaly of stream s by the calling
-// workgroup (TM_NT threads), LDS at `lds` (tm_layout).
-// Bind the LDS regions and stream s's buffers: the model (SP, segment pool,
-// frozen index) of stream s (the fleet's shared instance), the per-stream
-// scratch (qualifying lists, backtrack backups) of stream `scr` -- a helper
-// replaying another stream's backtrack uses its own scratch.
-template <bool LEARN, bool FROZEN>
-__device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b, int s, int scr, uint8_t* lds) {
-    const TmLayout L = tm_layout(c, LEARN, FROZEN);
-    t.c = c;
-    t.s = s;
-    t.sh = reinterpret_cast<TmSh*>(lds);
-    uint32_t* bmr = reinterpret_cast<uint32_t*>(lds + L.off_bm);
-    t.infA = bmr;
-    t.infP = bmr + c.cw;
-    t.infP1 = bmr + 2 * c.cw;
-    t.lrnA = LEARN ? bmr + 3 * c.cw : nullptr;
-    t.lrnA1 = LEARN ? bmr + 4 * c.cw : nullptr;
-    t.lrnP = LEARN ? bmr + 5 * c.cw : nullptr;
-    t.lrnP1 = LEARN ? bmr + 6 * c.cw : nullptr;
-    t.colconf = reinterpret_cast<float*>(lds + L.off_conf);
-    t.flags = reinterpret_cast<uint32_t*>(lds + L.off_flags);
-    t.U = reinterpret_cast<uint32_t*>(lds + L.off_U);
-    t.lrnpat = LEARN ? reinterpret_cast<uint16_t(*)[HTM_MAXACT]>(lds + L.off_lpat) : nullptr;
-    const size_t sc = (size_t)c.seg_cap;
-    // model buffers: the stream's own, or the fleet's shared instance 0
-    // (frozen inference writes only the segments' dutyCycle cache, with the
-    // value every stream computes for it, so sharing is race-free)
-    const size_t ms = (size_t)model_stream(c, s);
-    t.meta = b.seg_meta + ms * sc;
-    t.src = b.seg_src + ms * sc * HTM_MAXSYN;
-    t.perm = b.seg_perm + ms * sc * HTM_MAXSYN;
-    t.conn = b.seg_conn + ms * sc;
-    t.duty = b.seg_duty + ms * sc * 3;
-    t.nseg = b.cell_nseg + ms * c.ncells;
-    t.upd = b.upd + ms * c.upd_cap;
-    t.sbm = b.scr_bm + (size_t)scr * 5 * c.cw;
-    t.sconf = b.scr_conf + (size_t)scr * c.ncol;
-    t.q1 = b.scr_q + (size_t)scr * c.q_cap;
-    t.q2 = b.scr_q2 + (size_t)scr * c.q_cap;
-    if (FROZEN) {
-        t.fxoff = b.fx_off + ms * (size_t)c.fx_noff;
-        t.fxent = b.fx_ent + b.fx_base[ms];
-        t.fxrec = b.fx_rec + ms * sc;
-        t.fxrslot = b.fx_rslot + ms * sc;
-        t.fxpcell = b.fx_pcell + ms * c.fx_pcap;
-        t.np = b.fx_np[ms];
-        t.nr = b.fx_nr[ms];
-    } else {
-        t.fxoff = nullptr;
-        t.fxent = nullptr;
-        t.fxrec = nullptr;
-        t.fxrslot = nullptr;
-        t.fxpcell = nullptr;
-        t.np = 0;
-        t.nr = 0;
-    }
-    t.tb = &b;
-    t.bt_epoch = 0;
-    t.defer = FROZEN && b.fx_dlog != nullptr;
-}
-
-// Write the inference state back to HBM, touching only what changed:
-// infActiveState words that differ from HBM (the old words are loaded first,
-// their latency hidden behind the colConfidence bitmap), infPredictedState
-// words that differ from infP(t-1) (on the first step of a run the LDS copy
-// is what HBM holds), and colConfidence sparsely: gnz[0..nw) is the
-// nonzero-column bitmap of the dense HBM copy, gnz[nw] == 1 says it is valid
-// (the host clears it whenever it changes the state), so only the columns
-// nonzero before or now are written.  Uses t.flags (free after the TM step).
-// Returns the bytes this thread moved.  Contains barriers.
-__device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint32_t* gbm, float* gconf,
-                                                         uint32_t* gnz) {
-    const DevCfg& c = t.c;
-    constexpr int PER = 4;  // old infA words prefetched per thread (all of them up to 32,768 cells)
-    uint32_t olda[PER];
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        olda[j] = w < c.cw ? gbm[w] : 0u;
-    }
-    uint32_t oldnz[(HTM_MAXNW + TM_NT - 1) / TM_NT];
-#pragma unroll
-    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        oldnz[j] = w < c.nw ? gnz[w] : 0u;
-    }
-    const bool valid = gnz[c.nw] == 1u;
-    uint32_t* nzb = t.flags;  // the new bitmap
-    uint32_t* ozb = t.U;      // the old one (the union is free after the step)
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        if (w < c.nw) ozb[w] = oldnz[j];
-    }
-    // nonzero-column bitmap of the LDS colConfidence (ballots over 64 columns)
-    for (int col0 = wave_id() * 64; col0 < c.ncol; col0 += TM_NT) {
-        const int col = col0 + lane_id();
-        const uint64_t bal = __ballot(col < c.ncol && t.colconf[col] != 0.0f);
-        if (lane_id() == 0) {
-            nzb[col0 >> 5] = (uint32_t)bal;
-            if (col0 + 32 < c.ncol) nzb[(col0 >> 5) + 1] = (uint32_t)(bal >> 32);
-        }
-    }
-    __syncthreads();
-    uint32_t wb = 4u * (uint32_t)c.cw / TM_NT;  // old infA words read
-    for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
-        const uint32_t nb = (nzb[col >> 5] >> (col & 31)) & 1u;
-        const uint32_t ob = valid ? (ozb[col >> 5] >> (col & 31)) & 1u : 1u;
-        if (nb | ob) {
-            gconf[col] = t.colconf[col];
-            wb += 4;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        if (w < c.nw && (!valid || oldnz[j] != nzb[w])) {
-            gnz[w] = nzb[w];
-            wb += 4;
-        }
-    }
-    if (threadIdx.x == 0 && !valid) gnz[c.nw] = 1u;
-    for (int j = 0; threadIdx.x + j * TM_NT < (uint32_t)c.cw; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        uint32_t o = 0;
-#pragma unroll
-        for (int i = 0; i < PER; i++)
-            if (i == j) o = olda[i];
-        if (j >= PER) o = gbm[w];
-        const uint32_t v = t.infA[w];
-        if (o != v) {
-            gbm[w] = v;
-            wb += 4;
-        }
-        const uint32_t p = t.infP[w];
-        if (!first || t.infP1[w] != p) {
-            gbm[c.cw + w] = p;
-            wb += 4;
-        }
-    }
-    return wb;
-}
-
-template <bool LEARN, bool FROZEN>
-// first / last: the step opens / closes a run of steps by this workgroup.
-// Between them the stream's TM state (cell bitmaps, colConfidence, header,
-// pattern history, RNG) stays in LDS: only the first step loads it from HBM
-// and only the last writes it back.  bt_epoch > 0: backtracks are assisted.
-__device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores,
-                                             int keep_prev, int s, uint8_t* lds, int first = 1, int last = 1,
-                                             uint32_t bt_epoch = 0) {
-    Tm t;
-    tm_bind<LEARN, FROZEN>(t, c, b, s, s, lds);
-    t.bt_epoch = bt_epoch;
-    TmSh* sh = t.sh;
-    if (threadIdx.x == 0) sh->p1_n = -1;  // (no phase 1 yet this step)
-#ifdef HTM_STAMPS
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < HTM_NSTAMP; k++) sh->st_acc[k] = sh->st_cnt[k] = 0;
-        sh->st_last = __builtin_amdgcn_s_memtime();
-        sh->st_start = sh->st_last;
-    }
-#endif
-    htm_tm_header* hdr = b.hdr + s;
-    uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
-    float* gconf = b.colconf + (size_t)s * c.ncol;
-    uint16_t* gpat = b.pat + (size_t)s * 2 * HTM_MAXPAT * HTM_MAXACT;
-    // ---- load state
-    if (!first) {
-        // continuing in LDS: t -> t-1 rotation of the predicted / learn states
-        if (threadIdx.x == 0) {
-            const uint32_t na = sp.nact[s];
-            sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
-            sh->bytes = 4ull;
-        }
-        if (threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
-        wg_copy(t.infP1, t.infP, c.cw);
-        if (LEARN) {
-            wg_copy(t.lrnA1, t.lrnA, c.cw);
-            wg_copy(t.lrnP1, t.lrnP, c.cw);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) sh->bytes += 2ull * sh->nA;
-    }
-    if (first && threadIdx.x == 0) {
-        sh->bytes_acc = 0;
-        sh->avg_dens = hdr->avg_input_density;
-        sh->avg_lsl = hdr->avg_learned_seq_length;
-        sh->lrn_iter = hdr->lrn_iter;
-        sh->iter = hdr->iter;
-        sh->pam = hdr->pam_counter;
-        sh->lsl = hdr->learned_seq_length;
-        sh->reset = hdr->reset_called;
-        sh->have_avg = hdr->have_avg_density;
-        sh->rf = hdr->rng_f;
-        sh->rr = hdr->rng_r;
-        sh->hwm = hdr->seg_hwm;
-        sh->nlive = hdr->seg_live;
-        sh->n_inf_pat = hdr->n_inf_pat;
-        sh->n_lrn_pat = hdr->n_lrn_pat;
-        sh->inf_head = hdr->inf_pat_head;
-        sh->lrn_head = hdr->lrn_pat_head;
-        sh->n_upd = hdr->n_upd;
-        sh->err = hdr->error;
-        sh->st[0] = hdr->stat_inf_phase2;
-        sh->st[1] = hdr->stat_inf_backtrack;
-        sh->st[2] = hdr->stat_lrn_phase2;
-        sh->st[3] = hdr->stat_lrn_backtrack;
-        uint32_t na = sp.nact[s];
-        sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
-    }
-    if (first && threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
-    if (first && threadIdx.x < HTM_MAXPAT) {
-        sh->inf_len[threadIdx.x] = hdr->inf_pat_len[threadIdx.x];
-        sh->lrn_len[threadIdx.x] = hdr->lrn_pat_len[threadIdx.x];
-    }
-    if (first && threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
-    __syncthreads();
-    // live pattern-history entries only (ring slots head .. head+n-1)
-    if (first) {
-        const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
-        for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
-            const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
-            if (k < ni) {
-                const int slot = (sh->inf_head + k) % HTM_MAXPAT;
-                if (a < sh->inf_len[slot]) sh->inf_pat[slot][a] = gpat[slot * HTM_MAXACT + a];
-            } else {
-                const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
-                if (a < sh->lrn_len[slot])
-                    t.lrnpat[slot][a] = gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a];
-            }
-        }
-        if (threadIdx.x == 0) {
-            unsigned long long pb = 0;
-            for (int k = 0; k < ni; k++) pb += 2ull * sh->inf_len[(sh->inf_head + k) % HTM_MAXPAT];
-            for (int k = 0; k < nl; k++) pb += 2ull * sh->lrn_len[(sh->lrn_head + k) % HTM_MAXPAT];
-            // header in/out, active list, bitmaps in (t-1), colConfidence in (active cols)
-            sh->bytes = pb + 2ull * sizeof(htm_tm_header) + 2ull * sh->nA + 4ull +
-                        (LEARN ? 3ull : 1ull) * 4ull * c.cw + 4ull * sh->nA;
-        }
-    }
-    if (first) {
-        wg_copy(t.infP1, gbm + c.cw, c.cw);  // infPredictedState t -> t-1
-        wg_copy(t.infP, gbm + c.cw, c.cw);
-        if (LEARN) {
-            wg_copy(t.lrnA1, gbm + 2 * c.cw, c.cw);  // lrnActiveState t -> t-1
-            wg_copy(t.lrnP1, gbm + 3 * c.cw, c.cw);  // lrnPredictedState t -> t-1
-            wg_copy(t.lrnA, gbm + 2 * c.cw, c.cw);
-            wg_copy(t.lrnP, gbm + 3 * c.cw, c.cw);
-        }
-    }
-    __syncthreads();
-    const int nA = sh->nA;
-    // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1)),
-    // from HBM on the first step of a run, from LDS after it
-    const float* pconf = first ? gconf : t.colconf;
-    uint32_t hit = 0;
-    for (int a = threadIdx.x; a < nA; a += TM_NT) hit += pconf[sh->act[a]] != 0.0f ? 1u : 0u;
-    if (keep_prev)
-        for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
-            b.prev_pred[(size_t)s * c.ncol + col] = pconf[col] != 0.0f ? 1 : 0;
-    hit = wg_sum(sh, hit);
-    if (threadIdx.x == 0) {
-        // computeRawAnomalyScore -> Real32 output
-        scores[s] = nA > 0 ? (float)((double)(nA - (int)hit) / (double)nA) : 0.0f;
-        if (LEARN) sh->lrn_iter++;
-        sh->iter++;
-        if (!sh->have_avg) {
-            sh->avg_dens = (double)nA;
-            sh->have_avg = 1;
-        } else {
-            sh->avg_dens = 0.99 * sh->avg_dens + 0.01 * (double)nA;
-        }
-    }
-    __syncthreads();
-    STAMP(t, SB_LOAD);
-    if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) compact_pool(t);
-    // ---- BacktrackingTM.compute(input, learn, infer=True)
-    update_inference<FROZEN>(t, first ? gbm + c.cw : nullptr);
-    STAMP(t, SB_BT);
-    if (LEARN) update_learning(t);
-    STAMP(t, SB_LEARN);
-    // ---- write back (last step of the run only)
-    __syncthreads();
-    if (!last) {
-        if (threadIdx.x == 0) {
-            sh->bytes_acc += sh->bytes;
-            sh->reset = 0;  // reset_called is consumed by the step after the reset
-        }
-#ifdef HTM_STAMPS
-        __syncthreads();
-        STAMP(t, SB_WB);
-        COUNT(t, SC_STEPS, 1);
-        if (threadIdx.x == 0) {
-            uint64_t x = (sh->st_last - sh->st_start) >> 16;
-            int hb = 0;
-            while (x && hb < 8) { hb++; x >>= 1; }
-            sh->st_cnt[SC_HIST + hb] += 1;
-            uint64_t* d = b.dbg + (size_t)s * 2 * HTM_NSTAMP;
-            for (int k = 0; k < HTM_NSTAMP; k++) {
-                d[k] += sh->st_acc[k];
-                d[HTM_NSTAMP + k] += sh->st_cnt[k];
-            }
-        }
-#endif
-        return;
-    }
-    // cell bitmaps: only the words that changed.  infA's previous words are
-    // re-read from HBM; on the first step of a run infP1 holds what HBM holds
-    uint32_t wb = write_back_inference(t, first, gbm, gconf, b.colnz + (size_t)s * (c.nw + 1));
-    if (LEARN) {
-        wg_copy(gbm + 2 * c.cw, t.lrnA, c.cw);
-        wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
-        if (threadIdx.x == 0) wb += 8 * c.cw;
-    }
-    // patterns: a single step changes only the slot it pushed (pops move
-    // the heads); a run of steps writes back every live slot
-    if (first) {
-        if (sh->ti[0] >= 0)
-            for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
-                gpat[sh->ti[0] * HTM_MAXACT + a] = sh->inf_pat[sh->ti[0]][a];
-        if (LEARN && sh->ti[1] >= 0)
-            for (int a = threadIdx.x; a < sh->nA; a += TM_NT)
-                gpat[(HTM_MAXPAT + sh->ti[1]) * HTM_MAXACT + a] = t.lrnpat[sh->ti[1]][a];
-    } else {
-        const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
-        for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
-            const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
-            if (k < ni) {
-                const int slot = (sh->inf_head + k) % HTM_MAXPAT;
-                if (a < sh->inf_len[slot]) gpat[slot * HTM_MAXACT + a] = sh->inf_pat[slot][a];
-            } else {
-                const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
-                if (a < sh->lrn_len[slot]) gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a] = t.lrnpat[slot][a];
-            }
-        }
-    }
-    wb = wg_sum(sh, wb);
-    if (threadIdx.x == 0) {
-        // bitmaps out (changed words; infA's old words read), colConfidence
-        // out (sparse), nonzero-column map, pushed patterns, score
-        sh->bytes += wb + (LEARN ? 4ull : 2ull) * sh->nA + 4ull;
-        hdr->stat_bytes += sh->bytes_acc + sh->bytes;
-    }
-    // the RNG moves only when learning; a single step changes one ring slot's length
-    if (LEARN && threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
-    if (threadIdx.x < HTM_MAXPAT) {
-        if (!first || (int)threadIdx.x == sh->ti[0]) hdr->inf_pat_len[threadIdx.x] = sh->inf_len[threadIdx.x];
-        if (LEARN && (!first || (int)threadIdx.x == sh->ti[1])) hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
-    }
-    if (threadIdx.x == 0) {
-        hdr->avg_input_density = sh->avg_dens;
-        hdr->avg_learned_seq_length = sh->avg_lsl;
-        hdr->lrn_iter = sh->lrn_iter;
-        hdr->iter = sh->iter;
-        hdr->pam_counter = sh->pam;
-        hdr->learned_seq_length = sh->lsl;
-        hdr->reset_called = 0;
-        hdr->have_avg_density = sh->have_avg;
-        hdr->rng_f = sh->rf;
-        hdr->rng_r = sh->rr;
-        hdr->seg_hwm = sh->hwm;
-        hdr->seg_live = sh->nlive;
-        hdr->n_inf_pat = sh->n_inf_pat;
-        hdr->n_lrn_pat = sh->n_lrn_pat;
-        hdr->inf_pat_head = (uint16_t)sh->inf_head;
-        hdr->lrn_pat_head = (uint16_t)sh->lrn_head;
-        hdr->n_upd = sh->n_upd;
-        hdr->error = sh->err;
-        hdr->stat_inf_phase2 = sh->st[0];
-        hdr->stat_inf_backtrack = sh->st[1];
-        hdr->stat_lrn_phase2 = sh->st[2];
-        hdr->stat_lrn_backtrack = sh->st[3];
-    }
-#ifdef HTM_STAMPS
-    __syncthreads();
-    STAMP(t, SB_WB);
-    COUNT(t, SC_STEPS, 1);
-    if (threadIdx.x == 0) {
-        uint64_t x = (sh->st_last - sh->st_start) >> 16;
-        int hb = 0;
-        while (x && hb < 8) { hb++; x >>= 1; }
-        sh->st_cnt[SC_HIST + hb] += 1;
-    }
-    if (threadIdx.x == 0 && b.dbg) {
-        uint64_t* d = b.dbg + (size_t)s * 2 * HTM_NSTAMP;
-        for (int k = 0; k < HTM_NSTAMP; k++) {
-            d[k] += sh->st_acc[k];
-            d[HTM_NSTAMP + k] += sh->st_cnt[k];
-        }
-    }
-#endif
-}
-
-template <bool LEARN, bool FROZEN>
-__global__ __launch_bounds__(TM_NT) void tm_step_kernel(DevCfg c, TmBufs b, SpBufs sp, float* scores, int keep_prev) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    tm_step_body<LEARN, FROZEN>(c, b, sp, scores, keep_prev, blockIdx.x, lds);
-}
-
-// Fused network.run(1) x n_steps: each work unit steps one stream through
-// encoder -> SP -> TM -> anomaly for up to unit_steps consecutive records,
-// its state LDS-resident between them (streams are independent; every
-// stream's result is the one per-step launches give).  The SP's LDS aliases
-// the TM union region, which is free between steps.
-//
-// Persistent work queue: a grid of at most (resident workgroups) dequeues
-// units u = block * n + stream in order from wq[0]; unit (s, b) waits until
-// wq[1 + s] -- stream s's completed blocks -- reaches b.  Its predecessor
-// (s, b - 1) was dequeued n units earlier by a running workgroup, so the
-// wait always ends; every workgroup exits once the counter passes the last
-// unit.  This balances streams of unequal cost (backtracks) and removes the
-// quantisation of n streams over the resident slots.  State handed between
-// units goes through HBM: agent-scope fences on both sides (the XCDs' L2s
-// are not coherent with each other).
-// A workgroup that finished its own stream helps with posted backtrack jobs:
-// it takes a start offset of an open job (bt_take), claims it (bt_claim),
-// replays it with its own LDS and scratch, and publishes the result.  It
-// returns when every owner of the launch is done -- or, while workgroups of
-// the launch still wait to be dispatched, as soon as it finds nothing to do
-// (its slot is theirs).  Owners never wait on an unclaimed offset, so no
-// wait depends on a workgroup that is not running.
-template <bool FROZEN>
-__device__ __forceinline__ void bt_helper(const DevCfg& c, const TmBufs& b, uint8_t* lds, const BtArgs& bt, int n,
-                                          int my_s) {
-    TmSh* sh = reinterpret_cast<TmSh*>(lds);
-    const uint32_t ep = bt.epoch;
-    const unsigned long long all = bt.base + (unsigned long long)n;
-    const size_t rw = 2 * (size_t)c.cw + (size_t)c.ncol;
-    for (;;) {
-        if (wave_id() == 0) {
-            int job = -1, k = -1, state = 0;
-            const unsigned long long done = __hip_atomic_load(&b.bt_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (done >= all) {
-                state = 2;
-            } else {
-                const unsigned long long started =
-                    __hip_atomic_load(&b.bt_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                state = started >= all ? 1 : 0;
-                // help only in the launch's tail (at most `tail` owners left): earlier,
-                // helpers share CUs with running owners and slow them more than they help
-                const unsigned long long tail = bt.pad >> 8;
-                const bool in_tail = state == 1 && all - done <= tail;
-                for (int base = 0; in_tail && base < n && job < 0; base += 64) {
-                    const int j = base + lane_id();
-                    const int sj = j < n ? (my_s + 1 + j) % n : 0;
-                    const unsigned long long v =
-                        j < n ? __hip_atomic_load(&b.bt_state[sj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                    const uint32_t npj = (uint32_t)(v & 0xFFFFull);
-                    uint64_t bal = __ballot(j < n && (uint32_t)(v >> 16) == ep && (v & 0xFFFFull) != BT_CLOSED);
-                    while (bal && job < 0) {
-                        const int l0 = __ffsll((unsigned long long)bal) - 1;
-                        bal &= bal - 1ull;
-                        const int cand = __shfl(sj, l0, 64);
-                        const uint32_t np = __shfl(npj, l0, 64);
-                        int kk = -1;
-                        if (lane_id() == 0) {
-                            // the job's words were published before its state: acquire them
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            for (;;) {
-                                const unsigned long long tk = atomicAdd(&b.bt_take[cand], 1ull);
-                                const uint32_t x = (uint32_t)(tk & 0xFFFFull);
-                                if ((uint32_t)(tk >> 16) != ep || x >= np || x >= HTM_MAXPAT) break;
-                                if (bt_try_claim(&b.bt_claim[(size_t)cand * HTM_MAXPAT + x], ep)) {
-                                    kk = (int)x;
-                                    break;
-                                }
-                            }
-                        }
-                        kk = __shfl(kk, 0, 64);
-                        if (kk >= 0) {
-                            job = cand;
-                            k = kk;
-                        }
-                    }
-                }
-            }
-            if (lane_id() == 0) {
-                sh->ti[5] = job;
-                sh->ti[6] = k;
-                sh->ti[7] = state;
-            }
-        }
-        __syncthreads();
-        const int job = sh->ti[5], k = sh->ti[6], state = sh->ti[7];
-        __syncthreads();
-        if (job < 0) {
-            if (state != 1) return;  // all owners done, or dispatch still pending: leave
-            if (threadIdx.x == 0) __builtin_amdgcn_s_sleep(127);
-            __syncthreads();
-            continue;
-        }
-        // ---- replay start offset k of stream `job` (model of job, scratch of my_s)
-        Tm t;
-        tm_bind<false, FROZEN>(t, c, b, job, my_s, lds);
-        const uint32_t* ji = b.bt_info + (size_t)job * BT_INFO_WORDS;
-        const uint16_t* jp = b.bt_pat + (size_t)job * HTM_MAXPAT * HTM_MAXACT;
-        const int np = (int)ji[0];
-        if (threadIdx.x == 0) {
-            sh->lrn_iter = ji[1];
-            sh->avg_dens = __longlong_as_double((long long)((unsigned long long)ji[2] | ((unsigned long long)ji[3] << 32)));
-            sh->n_inf_pat = np;
-            sh->inf_head = 0;
-            sh->bytes = 0;
-            sh->st[0] = 0;
-            sh->err = 0;
-        }
-        if (threadIdx.x < HTM_MAXPAT) sh->inf_len[threadIdx.x] = threadIdx.x < np ? (uint16_t)ji[4 + threadIdx.x] : 0;
-        __syncthreads();
-        for (int i = threadIdx.x; i < np * HTM_MAXACT; i += TM_NT) {
-            const int kk = i / HTM_MAXACT, a = i % HTM_MAXACT;
-            if (a < sh->inf_len[kk]) sh->inf_pat[kk][a] = jp[i];
-        }
-        __syncthreads();
-        const bool inSeq = bt_replay<FROZEN>(t, k, np);
-        const size_t slot = (size_t)job * HTM_MAXPAT + k;
-        if (inSeq) {
-            uint32_t* rs = b.bt_res + slot * rw;
-            wg_copy(rs, t.infA, c.cw);
-            wg_copy(rs + c.cw, t.infP, c.cw);
-            wg_copy(rs + 2 * c.cw, reinterpret_cast<const uint32_t*>(t.colconf), c.ncol);
-        }
-        if (threadIdx.x == 0) {
-            uint32_t* mt = b.bt_meta + slot * 4;
-            mt[0] = (uint32_t)sh->bytes;
-            mt[1] = (uint32_t)(sh->bytes >> 32);
-            mt[2] = sh->st[0];
-            mt[3] = sh->err;
-        }
-        bt_release_store(&b.bt_claim[slot], ((unsigned long long)ep << 2) | (inSeq ? 2ull : 3ull));
-    }
-}
-
-template <bool LEARN, bool FROZEN, bool PAGED_OK>
-__device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
-                                             float* scores, int n_steps, int sp_learn, int keep_prev,
-                                             int keep_overlaps, uint32_t* wq, int unit_steps, int n, BtArgs bt) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t unit_sh[3];  // unit, its stream, its block
-    SpShared& ssh = *reinterpret_cast<SpShared*>(lds + tm_layout(c, LEARN, FROZEN).off_U);
-    const uint32_t nblk = (uint32_t)((n_steps + unit_steps - 1) / unit_steps);
-    const uint32_t total = (uint32_t)n * nblk;
-    // one flat loop over (unit, step) so the compiler sees the same single
-    // step loop as a one-stream run (no invariants hoisted across units)
-    // one unit per stream (n_steps <= unit_steps, e.g. every htm_step): no
-    // hand-offs, so no queue and no fences -- workgroup b runs stream b
-    const bool direct = nblk == 1;
-    // backtrack assist: frozen single-step (lockstep) launches only
-    const uint32_t bt_ep = (FROZEN && direct && b.bt_state) ? bt.epoch : 0u;
-    if (bt_ep && threadIdx.x == 0) atomicAdd(&b.bt_ctl[0], 1ull);
-    uint32_t u = 0xFFFFFFFFu;
-    int s = 0, k = 0, k0 = 0, k1 = 0;
-    for (;;) {
-        if (k == k1 && direct) {
-            if (u != 0xFFFFFFFFu || blockIdx.x >= (uint32_t)n) break;
-            u = blockIdx.x;
-            s = (int)blockIdx.x;
-            k0 = k = 0;
-            k1 = n_steps;
-        }
-        if (k == k1) {
-            if (u != 0xFFFFFFFFu) {
-                __threadfence();  // release this unit's state writes
-                __syncthreads();
-                if (threadIdx.x == 0)
-                    __hip_atomic_store(&wq[1 + s], (uint32_t)(k0 / unit_steps) + 1u, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (threadIdx.x == 0) {
-                const uint32_t x = atomicAdd(&wq[0], 1u);
-                if (x < total && x >= (uint32_t)n) {
-                    const uint32_t xs = x % (uint32_t)n, blk = x / (uint32_t)n;
-                    while (__hip_atomic_load(&wq[1 + xs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < blk)
-                        __builtin_amdgcn_s_sleep(8);
-                }
-                unit_sh[0] = x;
-                unit_sh[1] = x % (uint32_t)n;
-                unit_sh[2] = x / (uint32_t)n;
-            }
-            __syncthreads();
-            // SGPR copies: the stream index must stay scalar (a VALU division
-            // result would move every per-stream address into VGPRs)
-            u = __builtin_amdgcn_readfirstlane(unit_sh[0]);
-            if (u >= total) break;
-            __threadfence();  // acquire the previous unit's state writes (all threads)
-            s = (int)__builtin_amdgcn_readfirstlane(unit_sh[1]);
-            k0 = (int)__builtin_amdgcn_readfirstlane(unit_sh[2]) * unit_steps;
-            k1 = n_steps - k0 < unit_steps ? n_steps : k0 + unit_steps;
-            k = k0;
-        }
-        const double* v = values + (size_t)k * c.n_streams * c.n_fields;
-        if (sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps);
-        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps);
-        __syncthreads();
-        tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
-                                    k == k1 - 1, bt_ep);
-        __syncthreads();
-        k++;
-    }
-    if (bt_ep && blockIdx.x < (uint32_t)n) {
-        __shared__ uint32_t stay;
-        if (threadIdx.x == 0) {
-            atomicAdd(&b.bt_ctl[1], 1ull);  // this owner is done
-            // the first BT_HELPERS finishers stay as helpers; the others leave at
-            // once (a crowd of idle pollers costs the owners more than it helps)
-            const unsigned long long slot = atomicAdd(&b.bt_ctl[2], 1ull) - bt.base;  // every owner counts
-            stay = (bt.pad & 1u) && slot < BT_HELPERS ? 1u : 0u;
-        }
-        __syncthreads();
-        if (stay) bt_helper<FROZEN>(c, b, lds, bt, n, (int)blockIdx.x);
-    }
-}
-
-// The frozen-inference kernel (the bench kernel) is compiled for HTM_RUN_WAVES
-// waves per SIMD (3: three 256-thread workgroups per CU, with the LDS budget
-// sized to match); the learning kernels keep the compiler's register choice.
-#ifndef HTM_RUN_WAVES
-#define HTM_RUN_WAVES 3
-#endif
-#define HTM_RUN_ARGS                                                                                          \
-    DevCfg c, TmBufs b, SpBufs sp, const double *values, float *scores, int n_steps, int sp_learn, int keep_prev, \
-        int keep_overlaps, uint32_t *wq, int unit_steps, int n, BtArgs bt
-#define HTM_RUN_PASS c, b, sp, values, scores, n_steps, sp_learn, keep_prev, keep_overlaps, wq, unit_steps, n, bt
-
-__global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_kernel(
-    HTM_RUN_ARGS) {
-    htm_run_body<false, true, false>(HTM_RUN_PASS);
-}
-// the same for engines with paged SP permanences (SP learning may page in rows)
-__global__ __launch_bounds__(TM_NT) void htm_run_frozen_paged_kernel(HTM_RUN_ARGS) {
-    htm_run_body<false, true, true>(HTM_RUN_PASS);
-}
-template <bool LEARN>
-__global__ __launch_bounds__(TM_NT) void htm_run_kernel(HTM_RUN_ARGS) {
-    htm_run_body<LEARN, false, true>(HTM_RUN_PASS);
-}
 
 static int run_grid(const void* fn, size_t lds, int total) {
     // resident workgroups: cached per (kernel, LDS size)
@@ -2858,7 +30,7 @@ static int run_grid(const void* fn, size_t lds, int total) {
 
 int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
                    int n_steps, int sp_learn, int tm_learn, int frozen, int keep_prev, int keep_overlaps, int n,
-                   uint32_t* wq, int unit_steps, BtArgs bt, hipStream_t st) {
+                   uint32_t* wq, int unit_steps, hipStream_t st) {
     if (n <= 0 || n_steps <= 0) return 0;
     if (unit_steps < 1) unit_steps = 1;
     size_t lds = tm_step_lds_bytes(c, tm_learn, frozen);
@@ -2867,32 +39,21 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     const int total = (int)(n * nblk);
     // a single unit per stream runs on the hardware dispatcher (grid = streams)
     if (nblk > 1 && hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
-    const void* fn = tm_learn ? (const void*)htm_run_kernel<true>
-                     : frozen ? (c.sp_paged ? (const void*)htm_run_frozen_paged_kernel : (const void*)htm_run_frozen_kernel)
-                              : (const void*)htm_run_kernel<false>;
+    const int which = tm_learn ? 0 : frozen ? (c.sp_paged ? 2 : 1) : 3;
+    const void* fn = which == 0 ? tmk_fn_run_learn() : which == 1 ? tmk_fn_run_frozen()
+                     : which == 2 ? tmk_fn_run_frozen_paged() : tmk_fn_run_infer();
     const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
-    if (tm_learn)
-        hipLaunchKernelGGL((htm_run_kernel<true>), dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
-    else if (frozen && c.sp_paged)
-        hipLaunchKernelGGL(htm_run_frozen_paged_kernel, dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
-    else if (frozen)
-        hipLaunchKernelGGL(htm_run_frozen_kernel, dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
-    else
-        hipLaunchKernelGGL((htm_run_kernel<false>), dim3(grid), dim3(TM_NT), lds, st, HTM_RUN_PASS);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    switch (which) {
+        case 0: return tmk_launch_run_learn(grid, lds, st, HTM_RUN_PASS);
+        case 1: return tmk_launch_run_frozen(grid, lds, st, HTM_RUN_PASS);
+        case 2: return tmk_launch_run_frozen_paged(grid, lds, st, HTM_RUN_PASS);
+        default: return tmk_launch_run_infer(grid, lds, st, HTM_RUN_PASS);
+    }
 }
 
 int launch_tm_step(const DevCfg& c, const TmBufs& b, const SpBufs& sp, float* scores, int learn, int frozen, int n,
                    hipStream_t st) {
-    size_t lds = tm_step_lds_bytes(c, learn, frozen);
-    if (learn) {
-        hipLaunchKernelGGL((tm_step_kernel<true, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, scores, 0);
-    } else if (frozen) {
-        hipLaunchKernelGGL((tm_step_kernel<false, true>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, scores, 0);
-    } else {
-        hipLaunchKernelGGL((tm_step_kernel<false, false>), dim3(n), dim3(TM_NT), lds, st, c, b, sp, scores, 0);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return tmk_launch_step(learn, frozen, n, tm_step_lds_bytes(c, learn, frozen), st, c, b, sp, scores);
 }
 
 // ---------------------------------------------------------------------------
@@ -3162,27 +323,12 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
 int tm_configure_lds(const DevCfg& c) {
     // the frozen variant may exceed the default 64 KiB dynamic LDS limit
     size_t b0 = tm_step_lds_bytes(c, 1, 0), b1 = tm_step_lds_bytes(c, 0, 1), b2 = tm_step_lds_bytes(c, 0, 0);
-    hipError_t e0 = hipFuncSetAttribute((const void*)tm_step_kernel<true, false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b0);
-    hipError_t e1 = hipFuncSetAttribute((const void*)tm_step_kernel<false, true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
-    hipError_t e2 = hipFuncSetAttribute((const void*)tm_step_kernel<false, false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
-    hipError_t e3 = hipFuncSetAttribute((const void*)htm_run_kernel<true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b0);
-    hipError_t e4 = hipFuncSetAttribute((const void*)htm_run_frozen_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
-    hipError_t e5 = hipFuncSetAttribute((const void*)htm_run_kernel<false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b2);
-    hipError_t e6 = hipFuncSetAttribute((const void*)htm_run_frozen_paged_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
-    hipError_t e7 = hipFuncSetAttribute((const void*)tm_fx_flush_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1);
+    int r = tmk_attr_step(b0, b1, b2);
+    r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1);
+    r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
+                 hipSuccess ? 0 : -1;
     (void)hipGetLastError();
-    return (e0 == hipSuccess && e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess && e4 == hipSuccess &&
-            e5 == hipSuccess && e6 == hipSuccess && e7 == hipSuccess)
-               ? 0
-               : -1;
+    return r ? -1 : 0;
 }
 
 // Deferred dutyCycle() writes of frozen lockstep launches (TmBufs::fx_dlog):
@@ -3193,20 +339,25 @@ int tm_configure_lds(const DevCfg& c) {
 // concurrently: the writes store the value every replay computes.  The bytes
 // are not added to the streams' counters (the step kernel's roofline counts
 // its own work).  tm_fx_flush_done_kernel then marks the entries flushed and
-// clears fx_fwork (zero at allocation) for the next flush.
+// clears fx_fwork[0] (zero at allocation) for the next flush.
+// The flush runs on its own stream beside later steps: it replays the entries
+// [fx_dflushed, fx_dsnap) -- fx_dsnap is the snapshot of fx_dn taken on the
+// step stream when the flush was enqueued -- and the steps only append to ring
+// slots outside that range (a step reads fx_dflushed, which moves only when
+// a flush is complete; a stale read leaves it fewer free slots, never more).
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
     const uint32_t total = (uint32_t)n * (uint32_t)c.fx_dcap;
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) job = atomicAdd(b.fx_fwork, 1u);
+        if (threadIdx.x == 0) job = atomicAdd(&b.fx_fwork[0], 1u);
         __syncthreads();
         const uint32_t j = __builtin_amdgcn_readfirstlane(job);
         if (j >= total) break;
         const int s = (int)(j / (uint32_t)c.fx_dcap);
         const uint32_t i = j % (uint32_t)c.fx_dcap;  // ring slot: entry n - 1 - d, d = (n - 1 - i) mod dcap
-        const uint32_t n = b.fx_dn[s], f = b.fx_dflushed[s];
+        const uint32_t n = b.fx_dsnap[s], f = b.fx_dflushed[s];
         if (n == f) continue;
         const uint32_t d = (n - 1u + (uint32_t)c.fx_dcap - i % (uint32_t)c.fx_dcap) % (uint32_t)c.fx_dcap;
         if (d > n - 1u - f) continue;  // slot holds no unflushed entry
@@ -3231,7 +382,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         collect_frozen(t, c.act_thr, FX_WIN);
         __syncthreads();
         if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)c.q_cap) {
-            atomicOr(&b.hdr[s].error, 16u);  // qualifying-list overflow, as in the step
+            atomicOr(&b.fx_fwork[1], 16u);  // qualifying-list overflow, as in the step (htm_status)
             sh->qn = c.q_cap;
         }
         __syncthreads();
@@ -3239,11 +390,23 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
     }
 }
 
-// after a flush: every logged entry is flushed; the work counter restarts
+// after a flush: every snapshot entry is flushed; the work counter restarts
 __global__ void tm_fx_flush_done_kernel(TmBufs b, int n) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < n) b.fx_dflushed[s] = b.fx_dn[s];
-    if (s == 0) *b.fx_fwork = 0u;
+    if (s < n) b.fx_dflushed[s] = b.fx_dsnap[s];
+    if (s == 0) b.fx_fwork[0] = 0u;
+}
+
+// the entries a flush enqueued now covers (on the step stream, after the steps)
+__global__ void tm_fx_snap_kernel(TmBufs b, int n) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) b.fx_dsnap[s] = b.fx_dn[s];
+}
+
+int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st) {
+    if (n <= 0 || !b.fx_dlog) return 0;
+    hipLaunchKernelGGL(tm_fx_snap_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {

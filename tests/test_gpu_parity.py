@@ -287,45 +287,3 @@ def test_run_units_equal_lockstep_steps(rt, unit):
         sa, sb = a.tm_states(s), b.tm_states(s)
         for k in sa:
             assert np.array_equal(sa[k], sb[k])
-
-
-def test_backtrack_assist_equals_serial_backtracks(rt, trained, traces):
-    """Frozen lockstep steps with the backtrack assist (workgroups that finished
-    their own stream replay other streams' backtrack start offsets in
-    parallel, HTM_OPT_BT_ASSIST) equal the serial _inferBacktrack loop: the
-    same scores, cell states, colConfidence, pattern histories -- and the same
-    work counters, which count the serial loop's replays."""
-    base, _ = trained
-    n, T = 384, 48
-    engs = []
-    for assist in (1, 0):
-        e = rt.HTMEngine(n, seg_capacity=72 * 1024)
-        for region in rt._lib.ST:
-            e.import_state(region, base.export_state(region, 0, 1), s0=0)
-        e.replicate(0)
-        e.set_learning(False, False)
-        e.set_option(rt._lib.OPT_BT_ASSIST, assist)
-        e.defer_duty(False)  # (assisted launches never defer: compare like with like)
-        engs.append(e)
-    rng = np.random.default_rng(17)
-    idx = (np.arange(T)[:, None] + 97 * np.arange(n)[None, :]) % len(traces["test"])
-    vals = np.clip(traces["test"][idx] + rng.integers(-2, 3, size=idx.shape), 0, 100).astype(np.float64)
-    c0 = [e.counters() for e in engs]
-    outs = [np.stack([e.step(torch.tensor(vals[k], device="cuda")).cpu().numpy() for k in range(T)]) for e in engs]
-    c1 = [e.counters() for e in engs]
-    assert np.array_equal(outs[0], outs[1])
-    for k in ["inf_phase2", "inf_backtracks"]:
-        assert c1[0][k] - c0[0][k] == c1[1][k] - c0[1][k], k
-    # algorithmic bytes: the same replays; only the backtrack scratch traffic differs
-    # (no candidate copies, the posted history and a helper's result instead)
-    ba, bs = c1[0]["tm_bytes"] - c0[0]["tm_bytes"], c1[1]["tm_bytes"] - c0[1]["tm_bytes"]
-    assert abs(ba - bs) <= 0.05 * bs
-    assert c1[0]["inf_backtracks"] - c0[0]["inf_backtracks"] > n  # the assist path ran
-    for s in [0, 1, n // 2, n - 1]:
-        a, b = engs[0].tm_states(s), engs[1].tm_states(s)
-        for k in a:
-            assert np.array_equal(a[k], b[k])
-        assert np.array_equal(engs[0].col_confidence(s), engs[1].col_confidence(s))
-        assert engs[0].tm_patterns(s) == engs[1].tm_patterns(s)
-    for e in engs:
-        e.status()
