@@ -7,6 +7,8 @@
  * 1.0.x, which is absent; semantics follow SURVEY.md
  * Appendix A and the NuPIC 1.0.x algorithms the reference instantiates:
  *   - ScalarEncoder           NetworkUtils.py:77-88        (Appendix A.1)
+ *   - RandomDistributedScalarEncoder  params/model.yaml:15-21 (the 32-cell
+ *     model.yaml shape; NuPIC 1.0.x nupic/encoders/random_distributed_scalar.py)
  *   - SpatialPooler (cpp)     NetworkUtils.py:26-41,126-136 (Appendix A.2)
  *   - BacktrackingTM(CPP)     NetworkUtils.py:44-64,140-153 (Appendix A.3)
  *   - computeRawAnomalyScore  read at NetworkModel.py:133 (Appendix A.4)
@@ -23,6 +25,13 @@
  *   - Segment duty-cycle pow(1-alpha, age) evaluated by binary
  *     exponentiation in double, rounded to float (deterministic; equals the
  *     correctly rounded powf except in double-rounding corner cases).
+ *   - SP boost factors exp(x) (std::exp(float) in updateBoostFactorsGlobal_)
+ *     evaluated in double by a fixed operation sequence, rounded to float
+ *     (exp_det; equals the correctly rounded expf except in double-rounding
+ *     corner cases).
+ *   - RDSE: Random::shuffle is the Fisher-Yates form of nupic.core's
+ *     Random.hpp (swap(first[0], first[getUInt32(n)]), n decreasing); Python
+ *     2's round() rounds halves away from zero.
  *
  * Build: cc -O2 -ffp-contract=off -fopenmp -shared -fPIC (oracle/Makefile).
  */
@@ -103,6 +112,33 @@ static void rng_sample(rng_t* g, const uint32_t* pop, uint32_t n, uint32_t* out,
     }
 }
 
+/* exp(x) in double by a fixed sequence of IEEE operations (range reduction by
+ * ln 2 in two parts, degree-13 Taylor polynomial, exact power-of-two
+ * scaling), rounded to float: the SP boost factor std::exp((Real)...) of
+ * updateBoostFactorsGlobal_.  The HIP engine evaluates the same sequence
+ * (sp_dev.h exp_det), so both agree bit for bit. */
+static float exp_det(float xf) {
+    const double x = (double)xf;
+    if (!(x == x)) return xf;
+    if (x > 88.8) return INFINITY;
+    if (x < -104.0) return 0.0f;
+    const double inv_ln2 = 1.4426950408889634, ln2_hi = 6.93147180369123816490e-01,
+                 ln2_lo = 1.90821492927058770002e-10;
+    const double kd = x * inv_ln2;
+    const int k = (int)(kd < 0.0 ? kd - 0.5 : kd + 0.5);
+    const double r = (x - (double)k * ln2_hi) - (double)k * ln2_lo;
+    static const double inv_fact[14] = {1.0, 1.0, 0.5, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+                                        1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+                                        1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0};
+    double p = inv_fact[13];
+    for (int i = 12; i >= 0; i--) p = p * r + inv_fact[i];
+    union { double d; uint64_t u; } sc;
+    sc.u = (uint64_t)(1023 + k) << 52;
+    return (float)(p * sc.d);
+}
+
+float orc_exp_det(float x) { return exp_det(x); }
+
 /* =====================================================================
  * ScalarEncoder (nupic.encoders.scalar; Appendix A.1), fields concatenated
  * in sorted name order by MultiEncoder (NetworkUtils.py:77-108).
@@ -137,6 +173,150 @@ static void enc_encode(const orc_params* p, const double* values, uint8_t* out) 
         if (b < 0) continue;
         for (int k = 0; k < p->enc_w; k++) out[f * p->enc_n + b + k] = 1;
     }
+}
+
+/* =====================================================================
+ * RandomDistributedScalarEncoder (NuPIC 1.0.x
+ * nupic/encoders/random_distributed_scalar.py), the encoder of the
+ * reference's model.yaml parameter set (ML/HTM/params/model.yaml:15-21).
+ * State per field: the bucket map (bucket index -> w bit positions, grown on
+ * demand one neighbour at a time), the index range [minIndex, maxIndex],
+ * the offset (the first value encoded), and the encoder's own
+ * nupic::Random(seed).
+ * ===================================================================== */
+typedef struct {
+    int32_t min_idx, max_idx, has_offset, num_tries;
+    double offset;
+    rng_t rng;
+    int32_t* map; /* [ORC_RDSE_BUCKETS][w] */
+} rdse_t;
+
+/* __init__ -> _initializeBucketMap(INITIAL_BUCKETS, offset=None): the middle
+ * bucket is _permutation(n)[0:w], numpy.arange(n) shuffled by Random.shuffle */
+static void rdse_init(const orc_params* p, rdse_t* r, uint64_t seed) {
+    const int n = p->enc_n, w = p->enc_w;
+    rng_seed(&r->rng, seed);
+    r->min_idx = r->max_idx = ORC_RDSE_BUCKETS / 2;
+    r->has_offset = 0;
+    r->offset = 0.0;
+    r->num_tries = 0;
+    r->map = (int32_t*)calloc((size_t)ORC_RDSE_BUCKETS * w, sizeof(int32_t));
+    uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+    for (int i = 0; i < n; i++) perm[i] = (uint32_t)i;
+    uint32_t left = (uint32_t)n;
+    for (int i = 0; i < n; i++, left--) {
+        const uint32_t j = rng_u32(&r->rng, left);
+        const uint32_t t = perm[i];
+        perm[i] = perm[i + j];
+        perm[i + j] = t;
+    }
+    for (int k = 0; k < w; k++) r->map[(size_t)r->min_idx * w + k] = (int32_t)perm[k];
+    free(perm);
+}
+
+static void rdse_copy(const orc_params* p, rdse_t* d, const rdse_t* s) {
+    *d = *s;
+    const size_t nb = (size_t)ORC_RDSE_BUCKETS * p->enc_w * sizeof(int32_t);
+    d->map = (int32_t*)malloc(nb);
+    memcpy(d->map, s->map, nb);
+}
+
+/* Python 2 round(): halves away from zero (exact: v - trunc(v) is exact) */
+static double round_half_away(double v) {
+    const double t = trunc(v);
+    const double fr = v - t;
+    if (fr >= 0.5) return t + 1.0;
+    if (fr <= -0.5) return t - 1.0;
+    return t;
+}
+
+/* getBucketIndices(x): maxBuckets/2 + int(round((x - offset) / resolution)),
+ * clipped to [0, maxBuckets); the first value seen becomes the offset; a
+ * missing value (NaN) is bucket None (-1) and does not set the offset */
+static int rdse_bucket(const orc_params* p, rdse_t* r, double x) {
+    if (isnan(x)) return -1;
+    if (!r->has_offset) {
+        r->offset = x;
+        r->has_offset = 1;
+    }
+    const double q = round_half_away((x - r->offset) / p->rdse_resolution);
+    double b = (double)(ORC_RDSE_BUCKETS / 2) + q;
+    if (b < 0.0) b = 0.0;
+    if (b > (double)(ORC_RDSE_BUCKETS - 1)) b = (double)(ORC_RDSE_BUCKETS - 1);
+    return (int)b;
+}
+
+/* _overlapOK(i, j, overlap) with _maxOverlap = 2 */
+static int rdse_overlap_ok(int w, int i, int j, int overlap) {
+    const int d = i > j ? i - j : j - i;
+    return d < w ? overlap == w - d : overlap <= 2;
+}
+
+/* _newRepresentationOK(newRep, newIndex): running overlap of newRep with every
+ * existing bucket, minIndex .. maxIndex (adjacent buckets differ in one
+ * position: (i-1) % w below the middle, i % w above) */
+static int rdse_rep_ok(const orc_params* p, const rdse_t* r, const int32_t* rep, const uint8_t* bin, int new_idx) {
+    const int w = p->enc_w, mid = ORC_RDSE_BUCKETS / 2;
+    (void)rep;
+    const int32_t* m = r->map;
+    int run = 0;
+    for (int k = 0; k < w; k++) run += bin[m[(size_t)r->min_idx * w + k]];
+    if (!rdse_overlap_ok(w, r->min_idx, new_idx, run)) return 0;
+    for (int i = r->min_idx + 1; i <= mid; i++) {
+        const int nb = (i - 1) % w;
+        run -= bin[m[(size_t)(i - 1) * w + nb]];
+        run += bin[m[(size_t)i * w + nb]];
+        if (!rdse_overlap_ok(w, i, new_idx, run)) return 0;
+    }
+    for (int i = mid + 1; i <= r->max_idx; i++) {
+        const int nb = i % w;
+        run -= bin[m[(size_t)(i - 1) * w + nb]];
+        run += bin[m[(size_t)i * w + nb]];
+        if (!rdse_overlap_ok(w, i, new_idx, run)) return 0;
+    }
+    return 1;
+}
+
+/* _newRepresentation(index, newIndex): the neighbour's bits with position
+ * newIndex % w redrawn (getUInt32(n)) until the bit is new to the neighbour
+ * and the overlap rules hold against every existing bucket */
+static void rdse_new_rep(const orc_params* p, rdse_t* r, int from, int new_idx) {
+    const int n = p->enc_n, w = p->enc_w;
+    int32_t* rep = r->map + (size_t)new_idx * w;
+    const int32_t* nbr = r->map + (size_t)from * w;
+    memcpy(rep, nbr, sizeof(int32_t) * (size_t)w);
+    const int ri = new_idx % w;
+    uint8_t* bin = (uint8_t*)malloc((size_t)n);
+    for (;;) {
+        const int32_t bit = (int32_t)rng_u32(&r->rng, (uint32_t)n);
+        rep[ri] = bit;
+        int in_nbr = 0;
+        for (int k = 0; k < w; k++) in_nbr |= nbr[k] == bit;
+        if (!in_nbr) {
+            memset(bin, 0, (size_t)n);
+            for (int k = 0; k < w; k++) bin[rep[k]] = 1;
+            if (rdse_rep_ok(p, r, rep, bin, new_idx)) break;
+        }
+        r->num_tries++;
+    }
+    free(bin);
+}
+
+/* mapBucketIndexToNonZeroBits(index): _createBucket grows the map one
+ * neighbour at a time towards the index (the recursion's order) */
+static const int32_t* rdse_bits(const orc_params* p, rdse_t* r, int idx) {
+    if (idx < r->min_idx) {
+        for (int i = r->min_idx - 1; i >= idx; i--) {
+            rdse_new_rep(p, r, r->min_idx, i);
+            r->min_idx = i;
+        }
+    } else if (idx > r->max_idx) {
+        for (int i = r->max_idx + 1; i <= idx; i++) {
+            rdse_new_rep(p, r, r->max_idx, i);
+            r->max_idx = i;
+        }
+    }
+    return r->map + (size_t)idx * p->enc_w;
 }
 
 /* =====================================================================
@@ -408,7 +588,7 @@ static void sp_compute(const orc_params* p, sp_t* sp, const uint8_t* input, int 
         /* updateBoostFactorsGlobal_ */
         float target = sp_density(p, sp);
         for (int c = 0; c < ncol; c++)
-            sp->boost[c] = expf((target - sp->active_dc[c]) * p->sp_boost_strength);
+            sp->boost[c] = exp_det((target - sp->active_dc[c]) * p->sp_boost_strength);
         /* isUpdateRound_: updateInhibitionRadius_ (global: constant) and
          * updateMinDutyCyclesGlobal_ */
         if (sp->iter % p->sp_update_period == 0) {
@@ -1332,6 +1512,8 @@ static void tm_reset(tm_t* tm) {
  * ===================================================================== */
 struct orc_model {
     orc_params p;
+    rdse_t rdse[4];
+    int32_t bucket[4];
     sp_t sp;
     tm_t tm;
     uint8_t* input;
@@ -1383,8 +1565,14 @@ orc_model* orc_create(const orc_params* p) {
         p->tm_max_syn_per_seg > ORC_MAXSYN || p->tm_new_syn_count > ORC_MAXSYN ||
         p->tm_cells_per_col > 64))
         return NULL;
+    if (p->enc_type == ORC_ENC_RDSE &&
+        (p->sdr_bits > 0 || p->enc_w < 1 || p->enc_w % 2 == 0 || p->enc_n <= 6 * p->enc_w || !(p->rdse_resolution > 0.0)))
+        return NULL;
     orc_model* m = (orc_model*)calloc(1, sizeof(orc_model));
     m->p = *p;
+    if (p->enc_type == ORC_ENC_RDSE)
+        for (int f = 0; f < p->n_fields; f++) rdse_init(&m->p, &m->rdse[f], p->rdse_seed);
+    for (int f = 0; f < 4; f++) m->bucket[f] = -1;
     sp_init(&m->p, &m->sp);
     tm_init(&m->p, &m->tm);
     m->input = (uint8_t*)calloc((size_t)m->sp.nin, 1);
@@ -1395,6 +1583,9 @@ orc_model* orc_create(const orc_params* p) {
 orc_model* orc_clone(const orc_model* s) {
     orc_model* m = (orc_model*)calloc(1, sizeof(orc_model));
     m->p = s->p;
+    if (s->p.enc_type == ORC_ENC_RDSE)
+        for (int f = 0; f < s->p.n_fields; f++) rdse_copy(&s->p, &m->rdse[f], &s->rdse[f]);
+    memcpy(m->bucket, s->bucket, sizeof(m->bucket));
     sp_copy(&m->sp, &s->sp);
     tm_copy(&m->p, &m->tm, &s->tm);
     m->input = (uint8_t*)malloc((size_t)s->sp.nin);
@@ -1407,6 +1598,8 @@ orc_model* orc_clone(const orc_model* s) {
 
 void orc_free(orc_model* m) {
     if (!m) return;
+    if (m->p.enc_type == ORC_ENC_RDSE)
+        for (int f = 0; f < m->p.n_fields; f++) free(m->rdse[f].map);
     sp_free(&m->sp);
     tm_free(&m->p, &m->tm);
     free(m->input);
@@ -1416,8 +1609,27 @@ void orc_free(orc_model* m) {
 
 static float step_after_encode(orc_model* m, int sp_learn, int tm_learn);
 
+/* RecordSensor -> MultiEncoder.encodeIntoArray: fields in sorted name order,
+ * each encoder's n bits */
+static void model_encode(orc_model* m, const double* values, uint8_t* out) {
+    const orc_params* p = &m->p;
+    if (p->enc_type != ORC_ENC_RDSE) {
+        enc_encode(p, values, out);
+        for (int f = 0; f < p->n_fields; f++) m->bucket[f] = enc_first_on_bit(p, f, values[f]);
+        return;
+    }
+    memset(out, 0, (size_t)p->n_fields * p->enc_n);
+    for (int f = 0; f < p->n_fields; f++) {
+        const int b = rdse_bucket(p, &m->rdse[f], values[f]);
+        m->bucket[f] = b;
+        if (b < 0) continue;
+        const int32_t* bits = rdse_bits(p, &m->rdse[f], b);
+        for (int k = 0; k < p->enc_w; k++) out[f * p->enc_n + bits[k]] = 1;
+    }
+}
+
 float orc_step(orc_model* m, const double* values, int sp_learn, int tm_learn) {
-    enc_encode(&m->p, values, m->input);
+    model_encode(m, values, m->input);
     return step_after_encode(m, sp_learn, tm_learn);
 }
 
@@ -1471,7 +1683,23 @@ void orc_tm_reset(orc_model* m) { tm_reset(&m->tm); }
 int orc_num_inputs(const orc_model* m) { return m->sp.nin; }
 int orc_num_cells(const orc_model* m) { return m->tm.ncells; }
 
-void orc_encode(const orc_model* m, const double* values, uint8_t* out) { enc_encode(&m->p, values, out); }
+void orc_encode(orc_model* m, const double* values, uint8_t* out) { model_encode(m, values, out); }
+
+int orc_bucket(const orc_model* m, int f) { return (f >= 0 && f < 4) ? m->bucket[f] : -1; }
+
+void orc_rdse_state(const orc_model* m, int f, int32_t* sc4, double* offset, int32_t* map) {
+    const rdse_t* r = &m->rdse[f];
+    if (m->p.enc_type != ORC_ENC_RDSE || f < 0 || f >= m->p.n_fields) return;
+    sc4[0] = r->min_idx;
+    sc4[1] = r->max_idx;
+    sc4[2] = r->has_offset;
+    sc4[3] = r->num_tries;
+    *offset = r->offset;
+    const int w = m->p.enc_w;
+    memset(map, 0, sizeof(int32_t) * (size_t)ORC_RDSE_BUCKETS * w);
+    for (int i = r->min_idx; i <= r->max_idx; i++)
+        memcpy(map + (size_t)i * w, r->map + (size_t)i * w, sizeof(int32_t) * (size_t)w);
+}
 
 int orc_active_columns(const orc_model* m, int32_t* out) {
     memcpy(out, m->sp.active_sorted, 4 * (size_t)m->sp.n_active);

@@ -79,7 +79,19 @@ typedef struct {
      * else [enc_minval, enc_maxval] */
     double field_minval[4];
     double field_maxval[4];
+    /* encoder type: ORC_ENC_SCALAR (0, NetworkUtils.py:77-88) or ORC_ENC_RDSE --
+     * NuPIC's RandomDistributedScalarEncoder, the encoder of the reference's
+     * model.yaml parameter set (ML/HTM/params/model.yaml:15-21: resolution 0.88,
+     * seed 1; NuPIC defaults w = enc_w = 21, n = enc_n = 400) */
+    int32_t enc_type;
+    int32_t pad0;
+    double rdse_resolution;
+    uint64_t rdse_seed;
 } orc_params;
+
+#define ORC_ENC_SCALAR 0
+#define ORC_ENC_RDSE 1
+#define ORC_RDSE_BUCKETS 1000   /* RandomDistributedScalarEncoder INITIAL_BUCKETS (maxBuckets) */
 
 #define ORC_VAR_SP_TIE_LOW       0x001u /* global inhibition: ties -> LOWER index (strict '>' admission) */
 #define ORC_VAR_SP_NO_TIEBREAKER 0x002u /* SP init draws no 2048-entry tieBreaker before the pools */
@@ -116,7 +128,7 @@ void orc_tm_output(const orc_model* m, uint8_t* out);
 /* ---- introspection (state dumps for parity tests) ---- */
 int orc_num_inputs(const orc_model* m);
 int orc_num_cells(const orc_model* m);
-void orc_encode(const orc_model* m, const double* values, uint8_t* out);
+void orc_encode(orc_model* m, const double* values, uint8_t* out);  /* (RDSE: advances the encoder) */
 /* active columns of the last step, ascending; returns count */
 int orc_active_columns(const orc_model* m, int32_t* out);
 /* columns with nonzero colConfidence before the last step (anomaly input) */
@@ -150,6 +162,15 @@ void orc_rng_stream(uint64_t seed, int n, uint32_t* out);
 void orc_rng_real64(uint64_t seed, int n, double* out);
 /* TM RNG state of a model (31 words + fptr + rptr) */
 void orc_tm_rng_state(const orc_model* m, uint32_t* out33);
+/* RDSE encoder state of field f: scalars {minIndex, maxIndex, has_offset,
+ * numTries}, *offset, and the bucket map rows [ORC_RDSE_BUCKETS][w] (rows
+ * outside [minIndex, maxIndex] are zero) */
+void orc_rdse_state(const orc_model* m, int f, int32_t* scalars4, double* offset, int32_t* map);
+/* bucket index of field f of the last encoded record (-1: missing) */
+int orc_bucket(const orc_model* m, int f);
+/* boost factor exp((target - activeDutyCycle) * boostStrength) as the SP
+ * computes it (a deterministic double evaluation rounded to float) */
+float orc_exp_det(float x);
 
 #ifdef __cplusplus
 }

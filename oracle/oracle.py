@@ -38,7 +38,28 @@ class OrcParams(ctypes.Structure):
         ("tm_seg_update_valid_duration", ctypes.c_int32), ("tm_seed", ctypes.c_uint64),
         ("variant", ctypes.c_uint32), ("sdr_bits", ctypes.c_int32),
         ("field_minval", ctypes.c_double * 4), ("field_maxval", ctypes.c_double * 4),
+        ("enc_type", ctypes.c_int32), ("pad0", ctypes.c_int32), ("rdse_resolution", ctypes.c_double),
+        ("rdse_seed", ctypes.c_uint64),
     ]
+
+
+ENC_SCALAR, ENC_RDSE = 0, 1
+RDSE_BUCKETS = 1000
+
+
+def model_yaml_params(**overrides) -> "OrcParams":
+    """The reference's unused OPF parameter set ML/HTM/params/model.yaml: RDSE
+    (resolution 0.88, seed 1, NuPIC defaults w 21 / n 400 -- OPF sets the SP's
+    inputWidth to the encoder width, :15-21,29), SP (:28-41: seed 1956,
+    potentialPct 0.85, synPermActiveInc 0.04, synPermInactiveDec 0.005,
+    boostStrength 3.0) and a 32-cell BacktrackingTM (:45-63: seed 1960,
+    activationThreshold 16, minThreshold 12, pamLength 1)."""
+    kw = dict(enc_type=ENC_RDSE, enc_n=400, enc_w=21, rdse_resolution=0.88, rdse_seed=1,
+              sp_seed=1956, sp_potential_pct=0.85, sp_perm_active_inc=0.04, sp_perm_inactive_dec=0.005,
+              sp_boost_strength=3.0, tm_cells_per_col=32, tm_seed=1960, tm_activation_threshold=16,
+              tm_min_threshold=12, tm_pam_length=1)
+    kw.update(overrides)
+    return default_params(**kw)
 
 
 _lib = None
@@ -97,6 +118,11 @@ def lib():
         L.orc_rng_stream.argtypes = [ctypes.c_uint64, ctypes.c_int, vp]
         L.orc_rng_real64.argtypes = [ctypes.c_uint64, ctypes.c_int, vp]
         L.orc_tm_rng_state.argtypes = [vp, vp]
+        L.orc_rdse_state.argtypes = [vp, ctypes.c_int, vp, vp, vp]
+        L.orc_bucket.argtypes = [vp, ctypes.c_int]
+        L.orc_bucket.restype = ctypes.c_int
+        L.orc_exp_det.argtypes = [ctypes.c_float]
+        L.orc_exp_det.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -159,6 +185,7 @@ class OracleModel:
         return out
 
     def encode(self, values) -> np.ndarray:
+        """MultiEncoder.encodeIntoArray (an RDSE advances its state, as NuPIC's does)."""
         v = np.ascontiguousarray(np.atleast_1d(np.asarray(values, dtype=np.float64)))
         out = np.zeros(self.n_inputs, np.uint8)
         lib().orc_encode(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), _ptr(out))
@@ -235,6 +262,22 @@ class OracleModel:
         out = np.zeros(33, np.uint32)
         lib().orc_tm_rng_state(self.h, _ptr(out))
         return out
+
+    def bucket(self, f: int = 0) -> int:
+        """Bucket index of field f of the last encoded record (-1: missing)."""
+        return lib().orc_bucket(self.h, f)
+
+    def rdse_state(self, f: int = 0) -> dict:
+        sc = np.zeros(4, np.int32)
+        off = np.zeros(1, np.float64)
+        m = np.zeros((RDSE_BUCKETS, self.params.enc_w), np.int32)
+        lib().orc_rdse_state(self.h, f, _ptr(sc), _ptr(off), _ptr(m))
+        return dict(min_idx=int(sc[0]), max_idx=int(sc[1]), has_offset=int(sc[2]), num_tries=int(sc[3]),
+                    offset=float(off[0]), map=m)
+
+
+def exp_det(x: float) -> np.float32:
+    return np.float32(lib().orc_exp_det(float(np.float32(x))))
 
 
 def step_batch(models, values: np.ndarray, sp_learn: bool, tm_learn: bool, n_threads: int = 0) -> np.ndarray:

@@ -89,6 +89,9 @@ struct htm_engine {
     hipEvent_t ev_logged = nullptr;   // step stream: the snapshot of the log counters
     hipEvent_t ev_flushed = nullptr;  // fstream: the last enqueued flush is complete
     bool flush_pending = false;       // ev_flushed not yet waited for by a step stream or the host
+    int32_t flush_mode = 0;           // 0: flush stream beside the steps; 1: on the step stream
+    int32_t flush_wg = 0;             // flush kernel grid cap (0: FX_FLUSH_WG)
+    int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
 };
 
 // lockstep launches between two flushes of the deferred log (the flush runs
@@ -432,6 +435,9 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (const char* env = std::getenv("HTM_RUN_UNIT")) e->run_unit = std::max(1, std::atoi(env));  // A/B knob
     if (const char* env = std::getenv("HTM_DEFER_DUTY")) e->defer = std::atoi(env) != 0;            // A/B knob
     if (const char* env = std::getenv("HTM_DEFER_FLUSH_EVERY")) e->flush_every = std::max(1, std::atoi(env));  // test knob
+    if (const char* env = std::getenv("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
+    if (const char* env = std::getenv("HTM_FLUSH_WG")) e->flush_wg = std::max(1, std::atoi(env));         // A/B knob
+    if (const char* env = std::getenv("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
         // shapes whose fixed LDS state leaves no room at 3 workgroups per CU
@@ -592,7 +598,13 @@ static int alloc_dlog(htm_engine* e) {
     ALLOC(e->tm.fx_dsnap, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
     ALLOC(e->tm.fx_fwork, uint32_t, 2);
-    HIP_TRY(hipStreamCreateWithFlags(&e->fstream, hipStreamNonBlocking));
+    if (e->flush_prio) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&e->fstream, hipStreamNonBlocking, least));
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&e->fstream, hipStreamNonBlocking));
+    }
     HIP_TRY(hipEventCreateWithFlags(&e->ev_logged, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_flushed, hipEventDisableTiming));
     ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * (size_t)d.max_act_cells);  // last: the "allocated" test
@@ -607,9 +619,15 @@ static int alloc_dlog(htm_engine* e) {
 static int flush_async(htm_engine* e, hipStream_t st) {
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
     if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
+    if (e->flush_mode == 1 || st == e->fstream) {
+        if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, st))
+            return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
+        e->defer_steps = 0;
+        return HTM_OK;
+    }
     HIP_TRY(hipEventRecord(e->ev_logged, st));
     HIP_TRY(hipStreamWaitEvent(e->fstream, e->ev_logged, 0));
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->fstream))
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, e->fstream))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(e->ev_flushed, e->fstream));
     e->defer_steps = 0;

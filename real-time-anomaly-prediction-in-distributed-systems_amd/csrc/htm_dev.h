@@ -357,7 +357,7 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
                    uint32_t* wq, int unit_steps, hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
-int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st);
 int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

@@ -409,12 +409,13 @@ int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st) {
     if (n <= 0 || !b.fx_dlog) return 0;
     const size_t lds = tm_step_lds_bytes(c, 0, 1);
     const int total = n * c.fx_dcap;
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
+    if (max_wg > 0 && grid > max_wg) grid = max_wg;
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;

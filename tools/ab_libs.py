@@ -30,6 +30,7 @@ ts = []
 for r in range(3):
     t0 = time.perf_counter()
     out = [eng.step(vals[16 + r * K + k]) for k in range(K)]
+    eng.flush()
     torch.cuda.synchronize()
     ts.append((time.perf_counter() - t0) / K * 1e3)
 h = float(torch.stack(out).double().sum().item())
