@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HTM_ABI_VERSION 3
+#define HTM_ABI_VERSION 4
 
 /* error codes */
 #define HTM_OK 0
@@ -68,7 +68,9 @@ typedef struct {
     float sp_perm_inactive_dec;  /* 0.0005 */
     float sp_min_pct_overlap_dc; /* 0.001 */
     int32_t sp_duty_cycle_period;/* 1000 */
-    float sp_boost_strength;     /* 0.0 (only 0 is supported: boost == 1) */
+    float sp_boost_strength;     /* 0.0 (NetworkUtils.py:41); model.yaml:41 uses 3.0:
+                                    boostFactors = exp((targetDensity - activeDutyCycle) * strength)
+                                    after every learning step, boosted overlaps select the winners */
     int32_t sp_stimulus_threshold; /* 0 */
     int32_t sp_update_period;    /* 50 */
     uint64_t sp_seed;            /* 2045 */
@@ -120,7 +122,22 @@ typedef struct {
      * error flag 32 (htm_status: HTM_E_CAPACITY, results invalid). */
     int32_t sp_perm_rows;
     int32_t reserved0;           /* 0 */
+    /* Encoder of every field: HTM_ENC_SCALAR (the reference's ScalarEncoder,
+     * NetworkUtils.py:77-88) or HTM_ENC_RDSE -- NuPIC's
+     * RandomDistributedScalarEncoder of the model.yaml parameter set
+     * (ML/HTM/params/model.yaml:15-21: resolution 0.88, seed 1; n = enc_n
+     * (NuPIC default 400), w = enc_w (21, odd), n > 6 w).  An RDSE is stateful
+     * per stream and field: its bucket map grows on demand and its offset is
+     * the first value it encodes (state region HTM_ST_ENC_RDSE). */
+    int32_t enc_type;
+    int32_t reserved1;           /* 0 */
+    double rdse_resolution;      /* 0.88 */
+    uint64_t rdse_seed;          /* 1; stream s uses rdse_seed + s * seed_stride */
 } htm_config;
+
+#define HTM_ENC_SCALAR 0
+#define HTM_ENC_RDSE 1
+#define HTM_RDSE_BUCKETS 1000    /* RandomDistributedScalarEncoder INITIAL_BUCKETS */
 
 typedef struct htm_engine htm_engine;
 
@@ -213,6 +230,9 @@ int htm_run_sdr(htm_engine* eng, int32_t n_steps, const uint32_t* d_sdr, float* 
 #define HTM_OUT_COL_CONFIDENCE 7   /* float [ncol]  colConfidence t (topDownOut) */
 #define HTM_OUT_TM_OUTPUT 8        /* uint32 bitmap [ncells/32] bottomUpOut = infP|infA */
 #define HTM_OUT_SP_OVERLAPS 9      /* int32 [ncol] SP overlaps of the last step */
+#define HTM_OUT_BUCKETS 10         /* int32 [4] the encoders' bucket index per field of the last
+                                      record (-1: missing value): the sensor's bucketIdxOut
+                                      (NetworkModel.py:88-95) */
 int htm_get_output(htm_engine* eng, int32_t which, void* d_dst, size_t bytes, void* stream);
 /* Bytes per stream of an output selector (0 if unknown). */
 size_t htm_output_bytes(const htm_engine* eng, int32_t which);
@@ -242,7 +262,14 @@ size_t htm_output_bytes(const htm_engine* eng, int32_t which);
                                   of columns without a pool row).  Importing it re-bases the
                                   stream (its permanences keep their values); importing 0
                                   bytes keeps the stream's own. */
-#define HTM_ST_COUNT 17
+#define HTM_ST_SP_BOOST 18     /* float [ncol] boostFactors (1.0 until a learning step with
+                                  boostStrength != 0) */
+#define HTM_ST_ENC_RDSE 19     /* RDSE engines (enc_type HTM_ENC_RDSE) only, else 0 bytes: per
+                                  field, int32 [64] {minIndex, maxIndex, has_offset, numTries,
+                                  offset (double, 2 words), nupic::Random state [31], fptr, rptr,
+                                  0...} then int16 [HTM_RDSE_BUCKETS][enc_w] bucket map rows
+                                  (rows outside [minIndex, maxIndex] are unused), padded to 16 B */
+#define HTM_ST_COUNT 19
 size_t htm_state_bytes(const htm_engine* eng, int32_t region);
 int htm_export_state(htm_engine* eng, int32_t region, int32_t stream_begin, int32_t n,
                      void* h_dst, size_t bytes);

@@ -30,12 +30,14 @@ HTM_E_IO = -4
 HTM_E_STATE = -5
 
 OUT = dict(active_columns=1, prev_pred_columns=2, inf_active=3, inf_predicted=4, lrn_active=5,
-           lrn_predicted=6, col_confidence=7, tm_output=8, sp_overlaps=9)
+           lrn_predicted=6, col_confidence=7, tm_output=8, sp_overlaps=9, buckets=10)
 # sp_perm_ckpt first: a paged engine imports its permanences against the
 # initial values of the checkpoints they came with (HTM_ST_SP_PERM_CKPT)
 ST = dict(sp_perm_ckpt=17, sp_connT=1, sp_potmask=2, sp_perm=3, sp_duty=4, sp_scalars=5, tm_header=6, tm_bitmaps=7,
           tm_colconf=8, tm_seg_meta=9, tm_seg_src=10, tm_seg_perm=11, tm_seg_conn=12, tm_seg_duty=13,
-          tm_cell_nseg=14, tm_patterns=15, tm_updates=16)
+          tm_cell_nseg=14, tm_patterns=15, tm_updates=16, sp_boost=18, enc_rdse=19)
+ENC_SCALAR, ENC_RDSE = 0, 1
+RDSE_BUCKETS = 1000
 OPT_FROZEN_INDEX = 1
 OPT_KEEP_PREV = 2
 OPT_KEEP_OVERLAPS = 3
@@ -69,6 +71,8 @@ class HtmConfig(ctypes.Structure):
         ("sdr_bits", ctypes.c_int32),
         ("field_minval", ctypes.c_double * 4), ("field_maxval", ctypes.c_double * 4),
         ("sp_perm_rows", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+        ("enc_type", ctypes.c_int32), ("reserved1", ctypes.c_int32), ("rdse_resolution", ctypes.c_double),
+        ("rdse_seed", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -207,6 +211,22 @@ def lib():
 def check(code: int):
     if code != HTM_OK:
         raise HtmError(code, lib().htm_last_error().decode(errors="replace"))
+
+
+# The reference's unused OPF parameter set, ML/HTM/params/model.yaml: the
+# RandomDistributedScalarEncoder (:15-21; NuPIC defaults w 21, n 400 -- OPF
+# sets the SP inputWidth to the encoder's width), SP (:28-41) with
+# boostStrength 3.0, and the 32-cell BacktrackingTM (:45-63)
+MODEL_YAML = dict(enc_type=ENC_RDSE, enc_n=400, enc_w=21, rdse_resolution=0.88, rdse_seed=1,
+                  sp_seed=1956, sp_potential_pct=0.85, sp_perm_active_inc=0.04, sp_perm_inactive_dec=0.005,
+                  sp_boost_strength=3.0, tm_cells_per_col=32, tm_seed=1960, tm_activation_threshold=16,
+                  tm_min_threshold=12, tm_pam_length=1)
+
+
+def model_yaml_config(**overrides) -> HtmConfig:
+    kw = dict(MODEL_YAML)
+    kw.update(overrides)
+    return default_config(**kw)
 
 
 def default_config(**overrides) -> HtmConfig:

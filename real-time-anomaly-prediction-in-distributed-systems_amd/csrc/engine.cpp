@@ -51,6 +51,15 @@ struct Region {
     bool model;  // part of the model (SP permanences/connections, TM segment pool): one instance in a fleet
 };
 
+// lockstep launches between two flushes of the deferred log, and the grid of
+// a flush that runs beside the steps: a few workgroups fill the gaps the
+// steps' tails leave; a full-width flush beside them takes the slots the next
+// step's workgroups need (measured on config 2, profiles/r03_flush: 1,024 /
+// every 8 0.319 ms per step, 64 / 8 0.251, 128 / 16 0.249, the round-2
+// full-width flush on the step stream every 32 steps 0.263)
+#define FLUSH_EVERY 16
+#define FLUSH_WG 128
+
 struct htm_engine {
     htm_config cfg;
     DevCfg dc;
@@ -90,14 +99,11 @@ struct htm_engine {
     hipEvent_t ev_flushed = nullptr;  // fstream: the last enqueued flush is complete
     bool flush_pending = false;       // ev_flushed not yet waited for by a step stream or the host
     int32_t flush_mode = 0;           // 0: flush stream beside the steps; 1: on the step stream
-    int32_t flush_wg = 0;             // flush kernel grid cap (0: FX_FLUSH_WG)
+    int32_t flush_wg = FLUSH_WG;      // grid of a flush beside the steps
     int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
+    size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
 };
 
-// lockstep launches between two flushes of the deferred log (the flush runs
-// beside the steps, so frequent small flushes keep the one a timed region or
-// a state read must wait for short)
-#define FLUSH_EVERY 8
 
 static int flush_deferred(htm_engine* e, hipStream_t st);
 static int flush_sync(htm_engine* e);
@@ -144,6 +150,9 @@ void htm_default_config(htm_config* c) {
     c->seg_capacity = 1 << 17;
     c->upd_capacity = 2048;
     c->seed_stride = 0;
+    c->enc_type = HTM_ENC_SCALAR;
+    c->rdse_resolution = 0.88;
+    c->rdse_seed = 1;
 }
 
 }  // extern "C"
@@ -158,11 +167,20 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
         if (c.enc_w < 1 || c.enc_w >= c.enc_n || c.enc_n * c.n_fields > 2048)
             return htm_fail(HTM_E_INVALID, "encoder n/w out of range");
         if (c.n_fields * c.enc_w >= 128) return htm_fail(HTM_E_INVALID, "n_fields*w must be < 128");
+        if (c.enc_type != HTM_ENC_SCALAR && c.enc_type != HTM_ENC_RDSE)
+            return htm_fail(HTM_E_INVALID, "enc_type must be HTM_ENC_SCALAR or HTM_ENC_RDSE");
+        // RandomDistributedScalarEncoder.__init__'s checks (w odd, n > 6 w,
+        // resolution > 0); n <= 500 w lets the init shuffle run in the map rows
+        if (c.enc_type == HTM_ENC_RDSE &&
+            (c.enc_w % 2 == 0 || c.enc_n <= 6 * c.enc_w || c.enc_n > (HTM_RDSE_BUCKETS / 2) * c.enc_w ||
+             !(c.rdse_resolution > 0.0)))
+            return htm_fail(HTM_E_INVALID, "RDSE needs an odd w, 6 w < n <= 500 w and resolution > 0");
     }
     if (c.sp_columns < 64 || c.sp_columns % 64 != 0 || c.sp_columns > 4096)
         return htm_fail(HTM_E_INVALID, "sp_columns must be a multiple of 64 in [64, 4096]");
     if (c.sp_num_active < 1 || c.sp_num_active > HTM_MAXACT) return htm_fail(HTM_E_INVALID, "sp_num_active must be 1..64");
-    if (c.sp_boost_strength != 0.0f) return htm_fail(HTM_E_INVALID, "only boostStrength 0 is supported");
+    if (!(c.sp_boost_strength >= 0.0f) || c.sp_boost_strength > 1000.0f)
+        return htm_fail(HTM_E_INVALID, "boostStrength must be in [0, 1000]");
     if (c.sp_stimulus_threshold < 0 || c.sp_stimulus_threshold > 127) return htm_fail(HTM_E_INVALID, "stimulus threshold");
     if (c.tm_cells_per_col < 2 || c.tm_cells_per_col > HTM_MAXK) return htm_fail(HTM_E_INVALID, "cells_per_col must be 2..32");
     if ((int64_t)c.sp_columns * c.tm_cells_per_col > 65536) return htm_fail(HTM_E_INVALID, "columns*cells must be <= 65536");
@@ -181,6 +199,9 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     if (c.upd_capacity < 1 || c.upd_capacity > 65535) return htm_fail(HTM_E_INVALID, "upd_capacity");
     std::memset(&d, 0, sizeof(d));
     d.n_fields = sdr ? 0 : c.n_fields;
+    d.enc_type = sdr ? HTM_ENC_SCALAR : c.enc_type;
+    d.rdse_res = c.rdse_resolution;
+    d.rdse_block = (int32_t)(RDSE_HDR_WORDS * 4 + round_up((size_t)HTM_RDSE_BUCKETS * c.enc_w * 2, 16));
     d.enc_n = c.enc_n;
     d.enc_w = c.enc_w;
     d.enc_clip = c.enc_clip;
@@ -211,6 +232,9 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     float density = (float)c.sp_num_active / (float)area;
     if (density > 0.5f) density = 0.5f;
     d.num_desired = (int32_t)(uint32_t)(density * (float)c.sp_columns);
+    // updateBoostFactorsGlobal_: the same target density (global inhibition)
+    d.sp_boost = c.sp_boost_strength;
+    d.sp_target = density;
     if (d.num_desired > HTM_MAXACT) return htm_fail(HTM_E_INVALID, "too many winners");
     d.stim_thr = c.sp_stimulus_threshold;
     d.dc_period = c.sp_duty_cycle_period;
@@ -282,6 +306,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     win = (win / gran) * gran;
     if (win < 1024) win = 1024;
     if (win > 64512) win = 64512;
+    if (const char* env = std::getenv("HTM_FX_WIN_MAX"))  // A/B knob: a narrower window (occupancy study)
+        win = std::min(win, (size_t)std::max(1024, std::atoi(env)) / 64 * 64);
     size_t capr = round_up((size_t)d.seg_cap, 64);
     if (win > capr) win = capr;
     d.fx_win = (int32_t)win;
@@ -338,6 +364,17 @@ static int allocate(htm_engine* e) {
     }
     ALLOC(e->sp.err, uint32_t, S);
     ALLOC(e->sp.duty, float, M * 2 * d.ncol);
+    ALLOC(e->sp.boost, float, M * d.ncol);
+    ALLOC(e->sp.enc_bucket, int32_t, S * 4);
+    const size_t rdse_per = d.enc_type == HTM_ENC_RDSE ? (size_t)d.n_fields * d.rdse_block : 0;
+    if (rdse_per) {
+        ALLOC(e->sp.rdse, uint8_t, S * rdse_per);
+        ALLOC(e->sp.rdse_seeds, uint64_t, S);
+    } else {
+        e->sp.rdse = nullptr;
+        e->sp.rdse_seeds = nullptr;
+    }
+    e->sp.enc_in = nullptr;
     ALLOC(e->sp.scalars, uint32_t, S * 4);
     ALLOC(e->sp.act, uint16_t, S * HTM_MAXACT);
     ALLOC(e->sp.nact, uint32_t, S);
@@ -375,6 +412,8 @@ static int allocate(htm_engine* e) {
     r[HTM_ST_SP_PERM] = {e->sp.perm, (size_t)d.ncol * d.n_potential * 4, true};
     r[HTM_ST_SP_PERM_CKPT] = {e->sp.ckpt, d.sp_paged ? (size_t)d.n_ckpt * SP_CKPT_WORDS * 4 : 0, true};
     r[HTM_ST_SP_DUTY] = {e->sp.duty, (size_t)2 * d.ncol * 4, true};
+    r[HTM_ST_SP_BOOST] = {e->sp.boost, (size_t)d.ncol * 4, true};
+    r[HTM_ST_ENC_RDSE] = {e->sp.rdse, rdse_per, false};
     r[HTM_ST_SP_SCALARS] = {e->sp.scalars, 16, false};
     r[HTM_ST_TM_HEADER] = {e->tm.hdr, sizeof(htm_tm_header), false};
     r[HTM_ST_TM_BITMAPS] = {e->tm.bm, (size_t)4 * d.cw * 4, false};
@@ -436,7 +475,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (const char* env = std::getenv("HTM_DEFER_DUTY")) e->defer = std::atoi(env) != 0;            // A/B knob
     if (const char* env = std::getenv("HTM_DEFER_FLUSH_EVERY")) e->flush_every = std::max(1, std::atoi(env));  // test knob
     if (const char* env = std::getenv("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
-    if (const char* env = std::getenv("HTM_FLUSH_WG")) e->flush_wg = std::max(1, std::atoi(env));         // A/B knob
+    if (const char* env = std::getenv("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
     if (const char* env = std::getenv("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
@@ -480,6 +519,12 @@ static int init_streams(htm_engine* e, const htm_config* cfg, int32_t n_streams,
     for (int s = 0; s < n_streams; s++) seeds[s] = cfg->sp_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
     HIP_TRY(hipMemcpy(e->sp.seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
     if (launch_sp_init(e->dc, e->sp, n_streams, 0)) return htm_fail(HTM_E_HIP, "sp_init launch failed");
+    if (e->sp.rdse) {
+        std::vector<uint64_t> rs((size_t)n_streams);
+        for (int s = 0; s < n_streams; s++) rs[s] = cfg->rdse_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
+        HIP_TRY(hipMemcpy(e->sp.rdse_seeds, rs.data(), rs.size() * 8, hipMemcpyHostToDevice));
+        if (launch_rdse_init(e->dc, e->sp, n_streams, 0)) return htm_fail(HTM_E_HIP, "rdse_init launch failed");
+    }
     for (int s = 0; s < n_streams; s++) seeds[s] = cfg->tm_seed + (uint64_t)s * (uint64_t)cfg->seed_stride;
     HIP_TRY(hipMalloc(dseeds, seeds.size() * 8));
     HIP_TRY(hipMemcpy(*dseeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
@@ -507,6 +552,7 @@ int htm_destroy(htm_engine* e) {
     (void)hipDeviceSynchronize();
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->tm.fx_ent) (void)hipFree(e->tm.fx_ent);
+    if (e->sp.enc_in) (void)hipFree(e->sp.enc_in);
     for (hipEvent_t x : e->ev_pool) (void)hipEventDestroy(x);
     if (e->ev_logged) (void)hipEventDestroy(e->ev_logged);
     if (e->ev_flushed) (void)hipEventDestroy(e->ev_flushed);
@@ -597,7 +643,8 @@ static int alloc_dlog(htm_engine* e) {
     ALLOC(e->tm.fx_dflushed, uint32_t, S);
     ALLOC(e->tm.fx_dsnap, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
-    ALLOC(e->tm.fx_fwork, uint32_t, 2);
+    ALLOC(e->tm.fx_fwork, uint32_t, 4);
+    ALLOC(e->tm.fx_fjobs, uint32_t, S * (size_t)d.fx_dcap);
     if (e->flush_prio) {
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -620,7 +667,7 @@ static int flush_async(htm_engine* e, hipStream_t st) {
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
     if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
     if (e->flush_mode == 1 || st == e->fstream) {
-        if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, st))
+        if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st))
             return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
         e->defer_steps = 0;
         return HTM_OK;
@@ -637,12 +684,17 @@ static int flush_async(htm_engine* e, hipStream_t st) {
 
 // Flush and order `st` after it: work enqueued on `st` afterwards sees every
 // record write of the steps enqueued before (stream-ordered, asynchronous).
+// The flush beside the steps, if one is running, is waited for; the entries
+// logged since are flushed on `st` itself, full width (nothing runs beside).
 static int flush_deferred(htm_engine* e, hipStream_t st) {
-    if (int r = flush_async(e, st)) return r;
     if (e->flush_pending) {
         HIP_TRY(hipStreamWaitEvent(st, e->ev_flushed, 0));
         e->flush_pending = false;
     }
+    if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
+    if (launch_tm_fx_snap(e->tm, e->n, st) || launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st))
+        return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
+    e->defer_steps = 0;
     return HTM_OK;
 }
 
@@ -736,6 +788,25 @@ static int prepare_step(htm_engine* e, hipStream_t st, int* frozen) {
     return HTM_OK;
 }
 
+// RDSE engines: the encoder kernel runs the streams' encoders through the
+// launch's n_steps records first (their buffer grows to the longest launch).
+static int encode_rdse(htm_engine* e, const double* d_values, int32_t n_steps, hipStream_t st) {
+    if (e->dc.enc_type != HTM_ENC_RDSE) return HTM_OK;
+    if ((size_t)n_steps > e->enc_cap) {
+        if (e->sp.enc_in) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(e->sp.enc_in));
+            e->bytes -= e->enc_cap * (size_t)e->n * ENC_LIST * 2;
+            e->sp.enc_in = nullptr;
+        }
+        HIP_TRY(hipMalloc(&e->sp.enc_in, (size_t)n_steps * e->n * ENC_LIST * 2));
+        e->enc_cap = (size_t)n_steps;
+        e->bytes += e->enc_cap * (size_t)e->n * ENC_LIST * 2;
+    }
+    if (launch_rdse_encode(e->dc, e->sp, d_values, n_steps, e->n, st)) return htm_fail(HTM_E_HIP, "rdse encode launch");
+    return HTM_OK;
+}
+
 // n_steps network.run(1) of every stream in one fused SP+TM launch.
 static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, hipStream_t st,
                      int frozen) {
@@ -753,6 +824,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     // the launch's tail (measured on config 2, profiles/r01_s4/ab_unit.txt:
     // 256-step launches best at 32, 2324-step launches flat over 48..96)
     const int32_t unit = e->run_unit > 0 ? e->run_unit : std::max(16, std::min(64, n_steps / 8));
+    if (int r = encode_rdse(e, d_values, n_steps, st)) return r;
     TmBufs tb = e->tm;
     // deferred dutyCycle() writes: frozen lockstep launches (one step)
     const bool defer = frozen && n_steps == 1 && e->defer;
@@ -783,6 +855,7 @@ static int step_unfused(htm_engine* e, const double* d_values, const uint32_t* d
         if (r) return r;
         HIP_TRY(hipEventRecord(ev[0], st));
     }
+    if (!d_sdr && encode_rdse(e, d_values, 1, st)) return HTM_E_HIP;
     if (d_sdr ? launch_sp_step_sdr(e->dc, e->sp, d_sdr, e->sp_learn, e->n, e->keep_overlaps, st)
               : launch_sp_step(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, st))
         return htm_fail(HTM_E_HIP, "sp_step launch");
@@ -976,6 +1049,7 @@ size_t htm_output_bytes(const htm_engine* e, int32_t which) {
         case HTM_OUT_TM_OUTPUT: return (size_t)d.cw * 4;
         case HTM_OUT_COL_CONFIDENCE: return (size_t)d.ncol * 4;
         case HTM_OUT_SP_OVERLAPS: return (size_t)d.ncol * 4;
+        case HTM_OUT_BUCKETS: return 16;
         default: return 0;
     }
 }
@@ -1011,6 +1085,10 @@ int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void
         case HTM_OUT_SP_OVERLAPS:
             if (!e->keep_overlaps) return htm_fail(HTM_E_STATE, "SP overlaps need htm_set_option(KEEP_OVERLAPS)");
             HIP_TRY(hipMemcpyAsync(d_dst, e->sp.overlaps, per * e->n, hipMemcpyDeviceToDevice, st));
+            return HTM_OK;
+        case HTM_OUT_BUCKETS:
+            if (d.sdr_in) return htm_fail(HTM_E_STATE, "an SDR-input engine has no encoder");
+            HIP_TRY(hipMemcpyAsync(d_dst, e->sp.enc_bucket, per * e->n, hipMemcpyDeviceToDevice, st));
             return HTM_OK;
     }
     return htm_fail(HTM_E_INVALID, "unknown output");
@@ -1143,13 +1221,14 @@ static int import_region(htm_engine* e, int32_t region, int32_t s0, int32_t n, c
     // no checkpoints (an export of a dense engine): the streams keep their own
     if (region == HTM_ST_SP_PERM_CKPT && (bytes == 0 || r.per_stream == 0)) return HTM_OK;
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "import buffer too small");
+    if (r.per_stream == 0) return HTM_OK;  // (a region this engine does not have, e.g. RDSE state)
     if (int rf = flush_sync(e)) return rf;
     HIP_TRY(hipDeviceSynchronize());
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_import(e, s0, n, h_src, nullptr, 0);
     if (rebase && e->dc.sp_paged && (region == HTM_ST_SP_PERM_CKPT || region == HTM_ST_SP_POTMASK))
         return paged_rebase_import(e, region, s0, n, h_src);
     HIP_TRY(hipMemcpy((uint8_t*)r.base + r.per_stream * s0, h_src, r.per_stream * n, hipMemcpyHostToDevice));
-    if (region >= HTM_ST_TM_HEADER) e->fx_valid = false;
+    if (region >= HTM_ST_TM_HEADER && region <= HTM_ST_TM_UPDATES) e->fx_valid = false;
     return invalidate_colnz(e, nullptr);
 }
 
@@ -1327,7 +1406,7 @@ int htm_status(htm_engine* e) {
 // save / load: "HTMAMD01", abi, config, n, learning flags, then regions --
 // the SP checkpoints first, so a paged engine's permanences are imported
 // against the initial values they were exported with
-static int save_order(int k) { return k == 0 ? HTM_ST_SP_PERM_CKPT : k; }
+static int save_order(int k) { return k == 0 ? HTM_ST_SP_PERM_CKPT : k < HTM_ST_SP_PERM_CKPT ? k : k + 1; }
 
 int htm_save(htm_engine* e, const char* path) {
     if (!e || !path) return htm_fail(HTM_E_INVALID, "bad arguments");

@@ -70,7 +70,18 @@ struct DevCfg {
     int32_t pool_stride;                  // floats per pool row: n_potential rounded up to 128 B
     int32_t pad0;
     uint64_t pool_rows;                   // rows in SpBufs::pool
+    // boosting (updateBoostFactorsGlobal_): strength (0: factors stay 1.0, the
+    // integer inhibition path) and the target density numActive / area
+    float sp_boost, sp_target;
+    // encoder: HTM_ENC_SCALAR or HTM_ENC_RDSE (then the active input bits of a
+    // step come from rdse_encode_kernel through SpBufs::enc_in)
+    int32_t enc_type;
+    int32_t rdse_block;                   // bytes of one field's RDSE state (header + bucket map)
+    double rdse_res;                      // RDSE resolution
 };
+
+#define ENC_LIST 128        // u16 words per (step, stream) encoded input list: count, then the bits
+#define RDSE_HDR_WORDS 64   // int32 words of an RDSE field header (HTM_ST_ENC_RDSE)
 
 #define SP_CKPT_COLS 8      // columns per SP-initialisation checkpoint (paged permanences)
 #define SP_CKPT_WORDS 64    // words per checkpoint: st[31], idx, pending draws buf[31], pad
@@ -98,6 +109,16 @@ struct SpBufs {
     unsigned long long* pool_next;  // [1] rows handed out
     uint32_t* ckpt;     // [S][n_ckpt][SP_CKPT_WORDS] RNG state at columns 0, 8, 16, ... of sp_init
     uint32_t* err;      // [S] SP error flags (SP_ERR_POOL)
+    float* boost;       // [S][ncol] boostFactors_ (1.0 at init)
+    // RDSE encoders (DevCfg::enc_type == HTM_ENC_RDSE): per stream, per field
+    // a block of rdse_block bytes (header int32[RDSE_HDR_WORDS], then the
+    // int16 [HTM_RDSE_BUCKETS][enc_w] bucket map); the encoded active-input
+    // lists of the steps of one launch [steps][S][ENC_LIST] (word 0 = count);
+    // the last record's bucket per field (HTM_OUT_BUCKETS)
+    uint8_t* rdse;
+    uint16_t* enc_in;
+    int32_t* enc_bucket;  // [S][4]
+    uint64_t* rdse_seeds; // [S] RDSE seed per stream
 };
 
 struct TmBufs {
@@ -157,7 +178,8 @@ struct TmBufs {
     uint32_t* fx_dflushed;         // [S] entries flushed
     uint32_t* fx_dsnap;            // [S] fx_dn when the running flush was enqueued (its upper bound)
     uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
-    uint32_t* fx_fwork;            // [2] flush work counter, flush error flags (16: qualifying-list overflow)
+    uint32_t* fx_fwork;            // [4] flush job counter, error flags (16: qualifying-list overflow), jobs
+    uint32_t* fx_fjobs;            // [S * fx_dcap] the running flush's entries (stream * fx_dcap + ring slot)
 };
 
 #define FX_FLUSH_WG 1024  // persistent workgroups of tm_fx_flush_kernel (each has its own scratch list)
@@ -324,6 +346,31 @@ __device__ __forceinline__ uint32_t ballot_rank(uint64_t ball) {
     return (uint32_t)__popcll(ball & m);
 }
 
+// exp(x) in double by a fixed sequence of IEEE operations (range reduction by
+// ln 2 in two parts, degree-13 Taylor polynomial, exact power-of-two scaling),
+// rounded to float: the SP boost factor exp((target - activeDutyCycle) *
+// strength) of updateBoostFactorsGlobal_.  oracle/htm_oracle.c exp_det runs
+// the same operations, so both agree bit for bit (and with the correctly
+// rounded expf wherever double rounding does not intervene).
+__device__ __forceinline__ float exp_det(float xf) {
+    const double x = (double)xf;
+    if (!(x == x)) return xf;
+    if (x > 88.8) return __int_as_float(0x7f800000);
+    if (x < -104.0) return 0.0f;
+    const double inv_ln2 = 1.4426950408889634, ln2_hi = 6.93147180369123816490e-01,
+                 ln2_lo = 1.90821492927058770002e-10;
+    const double kd = __dmul_rn(x, inv_ln2);
+    const int k = (int)(kd < 0.0 ? __dadd_rn(kd, -0.5) : __dadd_rn(kd, 0.5));
+    const double r = __dadd_rn(__dadd_rn(x, -__dmul_rn((double)k, ln2_hi)), -__dmul_rn((double)k, ln2_lo));
+    const double inv_fact[14] = {1.0, 1.0, 0.5, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+                                 1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+                                 1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0};
+    double p = inv_fact[13];
+#pragma unroll
+    for (int i = 12; i >= 0; i--) p = __dadd_rn(__dmul_rn(p, r), inv_fact[i]);
+    return (float)__dmul_rn(p, __longlong_as_double((long long)(1023 + k) << 52));
+}
+
 // pow(b, e) for integer e by binary exponentiation in double, rounded to
 // float: deterministic on host and device (the oracle uses the same rule).
 __device__ __forceinline__ float pow_det(float b, uint32_t e) {
@@ -346,6 +393,8 @@ int launch_sp_perm_import(const DevCfg& c, const SpBufs& b, const float* src, si
                           hipStream_t st);
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                    hipStream_t st);
+int launch_rdse_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st);
+int launch_rdse_encode(const DevCfg& c, const SpBufs& b, const double* values, int n_steps, int n, hipStream_t st);
 int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,
                        hipStream_t st);
 int launch_tm_fx_rank(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

@@ -135,6 +135,8 @@ __global__ void sp_init_kernel(DevCfg c, SpBufs b, uint32_t* connC, int s0, int 
     sc[1] = 0;
     sc[2] = 0;  // min overlap duty cycle (float 0.0)
     sc[3] = 0;
+    float* bf = b.boost + (size_t)s * c.ncol;  // boostFactors_ start at 1.0
+    for (int col = 0; col < c.ncol; col++) bf[col] = 1.0f;
 }
 
 // connT[s][i][w] bit (col & 31) = connC[s][col][i / 32] bit (i & 31), w = col / 32:
@@ -278,9 +280,11 @@ int launch_sp_perm_import(const DevCfg& c, const SpBufs& b, const float* src, si
 
 // ---------------------------------------------------------------------------
 template <bool LEARN>
-__global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps) {
+__global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps,
+                                                      const uint16_t* enc) {
     __shared__ SpShared sh;
-    sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps);
+    __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
+    sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps, LEARN ? bkey : nullptr, enc);
 }
 
 // Level-2 SP of Models 2/3 (SPRegion fed an SDR, MultiLevelNetworkModel.py:92-95):
@@ -288,7 +292,8 @@ __global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const 
 template <bool LEARN>
 __global__ __launch_bounds__(256) void sp_step_sdr_kernel(DevCfg c, SpBufs b, const uint32_t* sdr, int write_overlaps) {
     __shared__ SpSharedSdr sh;
-    sp_step_body<LEARN>(c, b, sdr, blockIdx.x, sh, write_overlaps);
+    __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
+    sp_step_body<LEARN>(c, b, sdr, blockIdx.x, sh, write_overlaps, LEARN ? bkey : nullptr);
 }
 
 int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,
@@ -302,9 +307,185 @@ int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, in
 
 int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                    hipStream_t st) {
+    const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? b.enc_in : nullptr;  // (one step: row 0)
     if (learn)
-        hipLaunchKernelGGL(sp_step_kernel<true>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps);
+        hipLaunchKernelGGL(sp_step_kernel<true>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps, enc);
     else
-        hipLaunchKernelGGL(sp_step_kernel<false>, dim3(n), dim3(64), 0, st, c, b, values, keep_overlaps);
+        hipLaunchKernelGGL(sp_step_kernel<false>, dim3(n), dim3(64), 0, st, c, b, values, keep_overlaps, enc);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// RandomDistributedScalarEncoder (DevCfg::enc_type == HTM_ENC_RDSE): NuPIC
+// 1.0.x nupic/encoders/random_distributed_scalar.py, the encoder of the
+// reference's model.yaml parameter set (ML/HTM/params/model.yaml:15-21),
+// restated as oracle/htm_oracle.c rdse_*.  Per stream and field the state is a
+// header (bucket index range, offset, numTries, the encoder's nupic::Random)
+// and the int16 bucket map [HTM_RDSE_BUCKETS][w].  The encoding of a record
+// depends on every earlier record of its stream (the offset is the first value
+// seen, buckets are created on demand with random draws), so one lane runs a
+// stream through the steps of a launch in order; streams run in parallel.  The
+// lists of active input bits go to SpBufs::enc_in for the SP kernels.
+enum { RH_MIN = 0, RH_MAX = 1, RH_HAS_OFF = 2, RH_TRIES = 3, RH_OFF = 4, RH_RNG = 6, RH_F = 37, RH_R = 38 };
+
+// nupic::Random on the header's state words (global memory, one lane)
+__device__ __forceinline__ uint32_t rdse_raw(int32_t* h) {
+    uint32_t* st = reinterpret_cast<uint32_t*>(h + RH_RNG);
+    int32_t f = h[RH_F], r = h[RH_R];
+    st[f] += st[r];
+    const uint32_t i = (st[f] >> 1) & 0x7fffffffu;
+    if (++f >= 31) { f = 0; ++r; }
+    else if (++r >= 31) { r = 0; }
+    h[RH_F] = f;
+    h[RH_R] = r;
+    return i;
+}
+// Random::getUInt32(max): raw draws are < 2^31 <= the rejection bound
+__device__ __forceinline__ uint32_t rdse_u32(int32_t* h, uint32_t max) { return rdse_raw(h) % max; }
+
+__device__ __forceinline__ double rdse_offset(const int32_t* h) {
+    return __hiloint2double(h[RH_OFF + 1], h[RH_OFF]);
+}
+
+// _overlapOK(i, j, overlap) with _maxOverlap = 2
+__device__ __forceinline__ bool rdse_overlap_ok(int w, int i, int j, int ov) {
+    const int d = i > j ? i - j : j - i;
+    return d < w ? ov == w - d : ov <= 2;
+}
+
+// _newRepresentation(from, new_idx) with _newRepresentationOK's running
+// overlap against every existing bucket (adjacent buckets differ in one
+// position: (i-1) % w below the middle bucket, i % w above)
+__device__ void rdse_new_rep(const DevCfg& c, int32_t* h, int16_t* map, int from, int new_idx, uint32_t* bin) {
+    const int n = c.enc_n, w = c.enc_w, mid = HTM_RDSE_BUCKETS / 2;
+    int16_t* rep = map + (size_t)new_idx * w;
+    const int16_t* nbr = map + (size_t)from * w;
+    for (int k = 0; k < w; k++) rep[k] = nbr[k];
+    const int ri = new_idx % w;
+    const int lo = h[RH_MIN], hi = h[RH_MAX];
+    for (;;) {
+        const int bit = (int)rdse_u32(h, (uint32_t)n);
+        rep[ri] = (int16_t)bit;
+        bool ok = true;
+        for (int k = 0; k < w && ok; k++) ok = nbr[k] != bit;
+        if (ok) {
+            for (int q = 0; q < (n + 31) / 32; q++) bin[q] = 0u;
+            for (int k = 0; k < w; k++) bin[rep[k] >> 5] |= 1u << (rep[k] & 31);
+            auto on = [&](int b) { return (int)((bin[b >> 5] >> (b & 31)) & 1u); };
+            int run = 0;
+            for (int k = 0; k < w; k++) run += on(map[(size_t)lo * w + k]);
+            ok = rdse_overlap_ok(w, lo, new_idx, run);
+            for (int i = lo + 1; ok && i <= mid; i++) {
+                const int nb = (i - 1) % w;
+                run += on(map[(size_t)i * w + nb]) - on(map[(size_t)(i - 1) * w + nb]);
+                ok = rdse_overlap_ok(w, i, new_idx, run);
+            }
+            for (int i = mid + 1; ok && i <= hi; i++) {
+                const int nb = i % w;
+                run += on(map[(size_t)i * w + nb]) - on(map[(size_t)(i - 1) * w + nb]);
+                ok = rdse_overlap_ok(w, i, new_idx, run);
+            }
+            if (ok) return;
+        }
+        h[RH_TRIES]++;
+    }
+}
+
+// __init__: nupic::Random(seed), the middle bucket = the first w of
+// numpy.arange(n) after Random.shuffle (swap(a[i], a[i + getUInt32(n - i)]));
+// the shuffle runs in the map's own rows (n <= 500 w: below the middle row)
+__global__ void rdse_init_kernel(DevCfg c, SpBufs b, int n_streams) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_streams * c.n_fields) return;
+    const int s = t / c.n_fields, f = t % c.n_fields;
+    uint8_t* blk = b.rdse + (size_t)t * c.rdse_block;
+    int32_t* h = reinterpret_cast<int32_t*>(blk);
+    int16_t* map = reinterpret_cast<int16_t*>(blk + RDSE_HDR_WORDS * 4);
+    const int n = c.enc_n, w = c.enc_w, mid = HTM_RDSE_BUCKETS / 2;
+    uint32_t st[31];
+    int32_t rf, rr;
+    rng_seed(st, rf, rr, b.rdse_seeds[s]);
+    for (int i = 0; i < 31; i++) h[RH_RNG + i] = (int32_t)st[i];
+    h[RH_F] = rf;
+    h[RH_R] = rr;
+    for (int i = 0; i < n; i++) map[i] = (int16_t)i;
+    for (int i = 0; i < n; i++) {
+        const int j = i + (int)rdse_u32(h, (uint32_t)(n - i));
+        const int16_t x = map[i];
+        map[i] = map[j];
+        map[j] = x;
+    }
+    for (int k = 0; k < w; k++) map[(size_t)mid * w + k] = map[k];
+    for (int i = 0; i < n && i < mid * w; i++) map[i] = 0;
+    h[RH_MIN] = h[RH_MAX] = mid;
+    h[RH_HAS_OFF] = 0;
+    h[RH_TRIES] = 0;
+    h[RH_OFF] = h[RH_OFF + 1] = 0;
+}
+
+int launch_rdse_init(const DevCfg& c, const SpBufs& b, int n, hipStream_t st) {
+    const int lanes = n * c.n_fields;
+    hipLaunchKernelGGL(rdse_init_kernel, dim3((lanes + 63) / 64), dim3(64), 0, st, c, b, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Python 2 round(): halves away from zero (v - trunc(v) is exact)
+__device__ __forceinline__ double round_half_away(double v) {
+    const double t = trunc(v);
+    const double fr = __dadd_rn(v, -t);
+    return fr >= 0.5 ? t + 1.0 : fr <= -0.5 ? t - 1.0 : t;
+}
+
+// encodeIntoArray for n_steps records of every stream: getBucketIndices (the
+// first value sets the offset; NaN is missing: no bits, offset untouched),
+// mapBucketIndexToNonZeroBits (the map grows one neighbour at a time towards
+// the bucket, the recursion's order)
+__global__ void rdse_encode_kernel(DevCfg c, SpBufs b, const double* values, int n_steps, int n_streams) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_streams) return;
+    const int nf = c.n_fields, w = c.enc_w;
+    uint32_t bin[64];  // newRep as a bitmap (n <= 2048 bits)
+    for (int k = 0; k < n_steps; k++) {
+        uint16_t* out = b.enc_in + ((size_t)k * n_streams + s) * ENC_LIST;
+        int cnt = 0;
+        for (int f = 0; f < nf; f++) {
+            const double x = values[((size_t)k * n_streams + s) * nf + f];
+            uint8_t* blk = b.rdse + ((size_t)s * nf + f) * c.rdse_block;
+            int32_t* h = reinterpret_cast<int32_t*>(blk);
+            int16_t* map = reinterpret_cast<int16_t*>(blk + RDSE_HDR_WORDS * 4);
+            int bkt = -1;
+            if (!isnan(x)) {
+                if (!h[RH_HAS_OFF]) {
+                    const long long bits = __double_as_longlong(x);
+                    h[RH_OFF] = (int32_t)(uint32_t)bits;
+                    h[RH_OFF + 1] = (int32_t)(uint32_t)(bits >> 32);
+                    h[RH_HAS_OFF] = 1;
+                }
+                double q = (double)(HTM_RDSE_BUCKETS / 2) +
+                           round_half_away(__ddiv_rn(__dadd_rn(x, -rdse_offset(h)), c.rdse_res));
+                q = q < 0.0 ? 0.0 : q > (double)(HTM_RDSE_BUCKETS - 1) ? (double)(HTM_RDSE_BUCKETS - 1) : q;
+                bkt = (int)q;
+                if (bkt < h[RH_MIN]) {
+                    for (int i = h[RH_MIN] - 1; i >= bkt; i--) {
+                        rdse_new_rep(c, h, map, h[RH_MIN], i, bin);
+                        h[RH_MIN] = i;
+                    }
+                } else if (bkt > h[RH_MAX]) {
+                    for (int i = h[RH_MAX] + 1; i <= bkt; i++) {
+                        rdse_new_rep(c, h, map, h[RH_MAX], i, bin);
+                        h[RH_MAX] = i;
+                    }
+                }
+                const int16_t* row = map + (size_t)bkt * w;
+                for (int j = 0; j < w; j++) out[1 + cnt++] = (uint16_t)(f * c.enc_n + row[j]);
+            }
+            if (k == n_steps - 1) b.enc_bucket[(size_t)s * 4 + f] = bkt;
+        }
+        out[0] = (uint16_t)cnt;
+    }
+}
+
+int launch_rdse_encode(const DevCfg& c, const SpBufs& b, const double* values, int n_steps, int n, hipStream_t st) {
+    hipLaunchKernelGGL(rdse_encode_kernel, dim3((n + 63) / 64), dim3(64), 0, st, c, b, values, n_steps, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -69,8 +69,18 @@ struct SpSharedSdr {
     }
 };
 
+// Boosted inhibition (learning with boostStrength != 0, boostOverlaps_ then
+// inhibitColumnsGlobal_ on the float32 products): bkey holds the stream's
+// boost factors as float bits in a padded transposed layout, bkey[j * (nw + 1)
+// + w] for column 32 w + j (lane-consecutive, so wave 0's accesses are
+// conflict-free); it is overwritten with boost * overlap.
+__device__ __forceinline__ uint32_t bkey_at(const DevCfg& c, int col) {
+    return (uint32_t)((col & 31) * (c.nw + 1) + (col >> 5));
+}
+
 template <class SH>
-__device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SH& sh, int write_overlaps) {
+__device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SH& sh, int write_overlaps,
+                                                   uint32_t* bkey = nullptr) {
     constexpr int NPL = SH::kPlanes;
     const int l = lane_id();
     const int nw = c.nw;
@@ -100,15 +110,71 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     uint32_t cand1 = (gt1 | eq1) & ((l + 64) < nw ? ~0u : 0u);
     uint32_t win0 = 0, win1 = 0;
     uint32_t need = (uint32_t)c.num_desired;
-    for (int k = NPL - 1; k >= 0; k--) {
-        uint32_t h0 = cand0 & p0[k], h1 = cand1 & p1[k];
-        uint32_t cnt = wave_sum_u32((uint32_t)(__popc(h0) + __popc(h1)));
-        if (cnt >= need) {
-            cand0 = h0; cand1 = h1;
-        } else {
-            win0 |= h0; win1 |= h1;
-            need -= cnt;
-            cand0 &= ~p0[k]; cand1 &= ~p1[k];
+    if (bkey) {
+        // boosted overlaps boost * (Real)overlap as float bits (non-negative
+        // floats order as their bits); eligible when >= stimulusThreshold
+        const uint32_t ks = (uint32_t)nw + 1u;
+        const float thr = (float)c.stim_thr;
+        cand0 = cand1 = 0;
+        for (int j = 0; j < 32; j++) {
+            if (l < nw) {
+                uint32_t ov = 0;
+#pragma unroll
+                for (int k = 0; k < NPL; k++) ov |= ((p0[k] >> j) & 1u) << k;
+                const float f = __uint_as_float(bkey[j * ks + l]) * (float)ov;
+                bkey[j * ks + l] = __float_as_uint(f);
+                if (f >= thr) cand0 |= 1u << j;
+            }
+            if (l + 64 < nw) {
+                uint32_t ov = 0;
+#pragma unroll
+                for (int k = 0; k < NPL; k++) ov |= ((p1[k] >> j) & 1u) << k;
+                const float f = __uint_as_float(bkey[j * ks + l + 64]) * (float)ov;
+                bkey[j * ks + l + 64] = __float_as_uint(f);
+                if (f >= thr) cand1 |= 1u << j;
+            }
+        }
+        // the num_desired-th largest eligible key: the largest T with at
+        // least `need` eligible keys >= T, built bit by bit from the top
+        uint32_t T = 0;
+        for (int bit = 30; bit >= 0; bit--) {
+            const uint32_t x = T | (1u << bit);
+            uint32_t cnt = 0;
+            for (int j = 0; j < 32; j++) {
+                if (((cand0 >> j) & 1u) && bkey[j * ks + l] >= x) cnt++;
+                if (((cand1 >> j) & 1u) && bkey[j * ks + l + 64] >= x) cnt++;
+            }
+            if (wave_sum_u32(cnt) >= need) T = x;
+        }
+        // above T: winners; equal to T: the ties the index order settles
+        uint32_t t0 = 0, t1 = 0;
+        for (int j = 0; j < 32; j++) {
+            if ((cand0 >> j) & 1u) {
+                const uint32_t kv = bkey[j * ks + l];
+                if (kv > T) win0 |= 1u << j;
+                else if (kv == T) t0 |= 1u << j;
+            }
+            if ((cand1 >> j) & 1u) {
+                const uint32_t kv = bkey[j * ks + l + 64];
+                if (kv > T) win1 |= 1u << j;
+                else if (kv == T) t1 |= 1u << j;
+            }
+        }
+        cand0 = t0;
+        cand1 = t1;
+        const uint32_t nwin = wave_sum_u32((uint32_t)(__popc(win0) + __popc(win1)));
+        need = nwin < need ? need - nwin : 0u;
+    } else {
+        for (int k = NPL - 1; k >= 0; k--) {
+            uint32_t h0 = cand0 & p0[k], h1 = cand1 & p1[k];
+            uint32_t cnt = wave_sum_u32((uint32_t)(__popc(h0) + __popc(h1)));
+            if (cnt >= need) {
+                cand0 = h0; cand1 = h1;
+            } else {
+                win0 |= h0; win1 |= h1;
+                need -= cnt;
+                cand0 &= ~p0[k]; cand1 &= ~p1[k];
+            }
         }
     }
     // ties at the threshold: the `need` highest column indices win.  Words
@@ -415,18 +481,27 @@ __device__ __forceinline__ void sp_count_iteration(const SpBufs& b, int s, SH& s
     sh.iter = it;
 }
 
-// Input stage, encoder: RecordSensor -> MultiEncoder.encodeIntoArray
+// Input stage, encoder: RecordSensor -> MultiEncoder.encodeIntoArray.  A
+// ScalarEncoder is computed here; RDSE engines read the list
+// rdse_encode_kernel made for this step (enc: [S][ENC_LIST], count first).
 template <bool LEARN>
 __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, const double* values, int s,
-                                              SpShared& sh) {
+                                              SpShared& sh, const uint16_t* enc = nullptr) {
     const int t = threadIdx.x;
     if (t < 64) sh.in[t] = 0;
     if (t == 0) {
         int n = 0;
-        for (int f = 0; f < c.n_fields; f++) {
-            int bkt = enc_first_on_bit(c, f, values[(size_t)s * c.n_fields + f]);
-            if (bkt < 0) continue;
-            for (int k = 0; k < c.enc_w; k++) sh.act_inputs[n++] = f * c.enc_n + bkt + k;
+        if (enc) {
+            const uint16_t* e = enc + (size_t)s * ENC_LIST;
+            n = e[0];
+            for (int k = 0; k < n; k++) sh.act_inputs[k] = e[1 + k];
+        } else {
+            for (int f = 0; f < c.n_fields; f++) {
+                int bkt = enc_first_on_bit(c, f, values[(size_t)s * c.n_fields + f]);
+                b.enc_bucket[(size_t)s * 4 + f] = bkt;
+                if (bkt < 0) continue;
+                for (int k = 0; k < c.enc_w; k++) sh.act_inputs[n++] = f * c.enc_n + bkt + k;
+            }
         }
         sh.n_act_inputs = n;
         sp_count_iteration<LEARN>(b, s, sh);
@@ -442,7 +517,7 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
 // past nin are ignored: the link carries exactly inputWidth elements)
 template <bool LEARN>
 __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int s,
-                                              SpSharedSdr& sh) {
+                                              SpSharedSdr& sh, const uint16_t* = nullptr) {
     const int pw = c.nin_pad >> 5;
     const uint32_t* row = sdr + (size_t)s * pw;
     for (int w = threadIdx.x; w < pw; w += blockDim.x) {
@@ -459,13 +534,21 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
 // `input` is the encoder values (SpShared) or the input SDR (SpSharedSdr).
 // PAGED_OK = false compiles the paged-permanence path out (kernels that
 // never run paged engines: the frozen-inference bench kernel).
+// bkey: LDS for the boosted inhibition, (nw + 1) * 32 words (used when
+// learning with boostStrength != 0); enc: RDSE engines' encoded lists of the step.
 template <bool LEARN, bool PAGED_OK = true, class SH, class IN>
 __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, const IN* input, int s,
-                                             SH& sh, int write_overlaps) {
+                                             SH& sh, int write_overlaps, uint32_t* bkey = nullptr,
+                                             const uint16_t* enc = nullptr) {
     const int t = threadIdx.x;
-    sp_load_input<LEARN>(c, b, input, s, sh);
+    const bool boosted = LEARN && bkey && c.sp_boost != 0.0f;
+    sp_load_input<LEARN>(c, b, input, s, sh, enc);
+    if (boosted) {  // boostFactors_ of the stream -> bkey (float bits)
+        const float* bf = b.boost + (size_t)model_stream(c, s) * c.ncol;
+        for (int col = t; col < c.ncol; col += blockDim.x) bkey[bkey_at(c, col)] = __float_as_uint(bf[col]);
+    }
     __syncthreads();
-    if (t < 64) sp_overlap_inhibit(c, b, s, sh, write_overlaps);
+    if (t < 64) sp_overlap_inhibit(c, b, s, sh, write_overlaps, boosted ? bkey : nullptr);
     __syncthreads();
     const int nact = sh.nact < HTM_MAXACT ? sh.nact : HTM_MAXACT;
     if (t < nact) b.act[(size_t)s * HTM_MAXACT + t] = sh.actlist[t];
@@ -483,6 +566,7 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     if (t == 0) sh.nbump = 0;
     __syncthreads();
     float mx = 0.0f;
+    float* bf = b.boost + (size_t)model_stream(c, s) * c.ncol;
     for (int col = t; col < c.ncol; col += blockDim.x) {
         float ov = (float)((sh.ovnz[col >> 5] >> (col & 31)) & 1u);
         float ac = (float)((sh.act[col >> 5] >> (col & 31)) & 1u);
@@ -490,13 +574,16 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
         float a = (adc[col] * pm1 + ac) / pf;
         odc[col] = o;
         adc[col] = a;
+        // updateBoostFactorsGlobal_ (after bumpUpWeakColumns_, which leaves the
+        // duty cycles alone): exp((targetDensity - activeDutyCycle) * strength)
+        if (c.sp_boost != 0.0f) bf[col] = exp_det((c.sp_target - a) * c.sp_boost);
         mx = o > mx ? o : mx;
         if (o < min_odc) {  // bumpUpWeakColumns_ candidates
             int k = atomicAdd(&sh.nbump, 1);
             sh.bump[k] = (uint16_t)col;
         }
     }
-    // boost factors: exp((target - activeDutyCycle) * 0) == 1 (boostStrength 0)
+    // (boostStrength 0: the factors stay exp(0) == 1)
     __syncthreads();
     const int nb = sh.nbump;
     if (nb > 0) {

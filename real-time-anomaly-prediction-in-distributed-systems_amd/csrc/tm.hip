@@ -39,14 +39,16 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     const int total = (int)(n * nblk);
     // a single unit per stream runs on the hardware dispatcher (grid = streams)
     if (nblk > 1 && hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
-    const int which = tm_learn ? 0 : frozen ? (c.sp_paged ? 2 : 1) : 3;
+    const int which = tm_learn ? 0 : frozen ? (c.sp_paged ? 2 : sp_learn ? 4 : 1) : 3;
     const void* fn = which == 0 ? tmk_fn_run_learn() : which == 1 ? tmk_fn_run_frozen()
-                     : which == 2 ? tmk_fn_run_frozen_paged() : tmk_fn_run_infer();
+                     : which == 2 ? tmk_fn_run_frozen_paged() : which == 4 ? tmk_fn_run_frozen_spl()
+                                                                              : tmk_fn_run_infer();
     const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
     switch (which) {
         case 0: return tmk_launch_run_learn(grid, lds, st, HTM_RUN_PASS);
         case 1: return tmk_launch_run_frozen(grid, lds, st, HTM_RUN_PASS);
         case 2: return tmk_launch_run_frozen_paged(grid, lds, st, HTM_RUN_PASS);
+        case 4: return tmk_launch_run_frozen_spl(grid, lds, st, HTM_RUN_PASS);
         default: return tmk_launch_run_infer(grid, lds, st, HTM_RUN_PASS);
     }
 }
@@ -324,7 +326,8 @@ int tm_configure_lds(const DevCfg& c) {
     // the frozen variant may exceed the default 64 KiB dynamic LDS limit
     size_t b0 = tm_step_lds_bytes(c, 1, 0), b1 = tm_step_lds_bytes(c, 0, 1), b2 = tm_step_lds_bytes(c, 0, 0);
     int r = tmk_attr_step(b0, b1, b2);
-    r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1);
+    r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1) |
+         tmk_attr_run_frozen_spl(b1);
     r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
                  hipSuccess ? 0 : -1;
     (void)hipGetLastError();
@@ -348,19 +351,16 @@ int tm_configure_lds(const DevCfg& c) {
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
-    const uint32_t total = (uint32_t)n * (uint32_t)c.fx_dcap;
+    const uint32_t total = b.fx_fwork[2];  // the job list (tm_fx_jobs_kernel, the launch before)
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) job = atomicAdd(&b.fx_fwork[0], 1u);
         __syncthreads();
-        const uint32_t j = __builtin_amdgcn_readfirstlane(job);
-        if (j >= total) break;
+        const uint32_t jj = __builtin_amdgcn_readfirstlane(job);
+        if (jj >= total) break;
+        const uint32_t j = b.fx_fjobs[jj];  // stream * dcap + ring slot
         const int s = (int)(j / (uint32_t)c.fx_dcap);
-        const uint32_t i = j % (uint32_t)c.fx_dcap;  // ring slot: entry n - 1 - d, d = (n - 1 - i) mod dcap
-        const uint32_t n = b.fx_dsnap[s], f = b.fx_dflushed[s];
-        if (n == f) continue;
-        const uint32_t d = (n - 1u + (uint32_t)c.fx_dcap - i % (uint32_t)c.fx_dcap) % (uint32_t)c.fx_dcap;
-        if (d > n - 1u - f) continue;  // slot holds no unflushed entry
+        const uint32_t i = j % (uint32_t)c.fx_dcap;
         Tm t;
         tm_bind<false, true>(t, c, b, s, s, lds);
         t.q1 = b.fx_fq + (size_t)blockIdx.x * c.q_cap;
@@ -390,11 +390,27 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
     }
 }
 
-// after a flush: every snapshot entry is flushed; the work counter restarts
+// before a flush (on the flush's stream): the entries [fx_dflushed, fx_dsnap)
+// of every stream as a compact job list, so the flush's workgroups claim
+// only real entries
+__global__ void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t f = b.fx_dflushed[s], p = b.fx_dsnap[s] - f;
+    if (!p) return;
+    const uint32_t base = atomicAdd(&b.fx_fwork[2], p);
+    const uint32_t dcap = (uint32_t)c.fx_dcap;
+    for (uint32_t d = 0; d < p; d++) b.fx_fjobs[base + d] = (uint32_t)s * dcap + (f + d) % dcap;
+}
+
+// after a flush: every snapshot entry is flushed; the counters restart
 __global__ void tm_fx_flush_done_kernel(TmBufs b, int n) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < n) b.fx_dflushed[s] = b.fx_dsnap[s];
-    if (s == 0) b.fx_fwork[0] = 0u;
+    if (s == 0) {
+        b.fx_fwork[0] = 0u;
+        b.fx_fwork[2] = 0u;
+    }
 }
 
 // the entries a flush enqueued now covers (on the step stream, after the steps)
@@ -416,6 +432,7 @@ int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipS
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
+    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;

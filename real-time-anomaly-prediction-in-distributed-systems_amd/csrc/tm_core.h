@@ -147,7 +147,8 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
                               1 + FX_OWN / 2
                         : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
-    size_t spw = (sizeof(SpShared) + 3) / 4;  // the fused kernels' SP step
+    // the fused kernels' SP step, and the boosted-inhibition keys after it
+    size_t spw = align16(sizeof(SpShared)) / 4 + (c.sp_boost != 0.0f ? ((size_t)c.nw + 1) * 32 : 0);
     size_t u = fin;
     if (spw > u) u = spw;
     if (keys > u) u = keys;
@@ -2424,13 +2425,17 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
 // quantisation of n streams over the resident slots.  State handed between
 // units goes through HBM: agent-scope fences on both sides (the XCDs' L2s
 // are not coherent with each other).
-template <bool LEARN, bool FROZEN, bool PAGED_OK>
+// SPL = false compiles SP learning out (the frozen bench kernel: inference only)
+template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true>
 __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
                                              float* scores, int n_steps, int sp_learn, int keep_prev,
                                              int keep_overlaps, uint32_t* wq, int unit_steps, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t unit_sh[3];  // unit, its stream, its block
     SpShared& ssh = *reinterpret_cast<SpShared*>(lds + tm_layout(c, LEARN, FROZEN).off_U);
+    uint32_t* bkey = c.sp_boost != 0.0f
+                         ? reinterpret_cast<uint32_t*>(lds + tm_layout(c, LEARN, FROZEN).off_U + align16(sizeof(SpShared)))
+                         : nullptr;
     const uint32_t nblk = (uint32_t)((n_steps + unit_steps - 1) / unit_steps);
     const uint32_t total = (uint32_t)n * nblk;
     // one flat loop over (unit, step) so the compiler sees the same single
@@ -2479,8 +2484,9 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
             k = k0;
         }
         const double* v = values + (size_t)k * c.n_streams * c.n_fields;
-        if (sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps);
-        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps);
+        const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? sp.enc_in + (size_t)k * c.n_streams * ENC_LIST : nullptr;
+        if (SPL && sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, bkey, enc);
+        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc);
         __syncthreads();
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
                                     k == k1 - 1);
@@ -2512,6 +2518,7 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
     int tmk_launch_##name(int grid, size_t lds, hipStream_t st, HTM_RUN_ARGS);                       \
     int tmk_attr_##name(size_t lds);
 TM_RUN_KERNEL_DECL(run_frozen)
+TM_RUN_KERNEL_DECL(run_frozen_spl)
 TM_RUN_KERNEL_DECL(run_frozen_paged)
 TM_RUN_KERNEL_DECL(run_learn)
 TM_RUN_KERNEL_DECL(run_infer)

@@ -1,5 +1,6 @@
-// tm_k_frozen.hip -- the frozen-inference kernel (the bench kernel): fused
-// encoder -> SP -> TM (frozen forward index) -> raw anomaly, learning off.
+// tm_k_frozen.hip -- the frozen-inference kernels: fused encoder -> SP -> TM
+// (frozen forward index) -> raw anomaly with TM learning off -- SP learning off
+// too (the bench kernel) or on (the reference's test phase).
 // Compiled for HTM_RUN_WAVES waves per SIMD (3: three 256-thread workgroups
 // per CU, with the LDS budget sized to match).  Kernel bodies: tm_core.h.
 #include "tm_core.h"
@@ -8,9 +9,16 @@
 #define HTM_RUN_WAVES 3
 #endif
 
+// inference only (SP learning off too): the bench kernel
 __global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_kernel(
     HTM_RUN_ARGS) {
-    htm_run_body<false, true, false>(HTM_RUN_PASS);
+    htm_run_body<false, true, false, false>(HTM_RUN_PASS);
+}
+// TM frozen, SP learning on (ModelTesting's test phase, NetworkModel.py:40-44)
+__global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_spl_kernel(
+    HTM_RUN_ARGS) {
+    htm_run_body<false, true, false, true>(HTM_RUN_PASS);
 }
 
 TM_RUN_KERNEL_EXPORTS(run_frozen, htm_run_frozen_kernel)
+TM_RUN_KERNEL_EXPORTS(run_frozen_spl, htm_run_frozen_spl_kernel)

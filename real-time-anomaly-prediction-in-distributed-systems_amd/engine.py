@@ -315,9 +315,28 @@ class HTMEngine:
         conn = np.unpackbits(connT.view(np.uint8).reshape(nin_pad, -1), axis=1, bitorder="little")[:nin, :c.sp_columns]
         duty = self.export_state("sp_duty", self._model_index(s), 1)[0].view(np.float32).reshape(2, c.sp_columns)
         sc = self.export_state("sp_scalars", s, 1)[0].view(np.uint32)
+        boost = self.export_state("sp_boost", self._model_index(s), 1)[0].view(np.float32).copy()
         return dict(perm=perm, potential=pot.astype(np.uint8), connected=conn.T.copy().astype(np.uint8),
-                    overlap_dc=duty[0].copy(), active_dc=duty[1].copy(),
+                    overlap_dc=duty[0].copy(), active_dc=duty[1].copy(), boost=boost,
                     min_overlap_dc=np.float32(sc[2:3].view(np.float32)[0]), iter=int(sc[0]), iter_learn=int(sc[1]))
+
+    def rdse_state(self, s: int, f: int = 0) -> dict:
+        """RDSE encoder state of field f of stream s in the layout of
+        oracle.OracleModel.rdse_state (bucket map rows outside the index range
+        zero)."""
+        c = self.config
+        if c.enc_type != _lib.ENC_RDSE:
+            raise ValueError("not an RDSE engine")
+        raw = self.export_state("enc_rdse", s, 1)[0]
+        blk = len(raw) // c.n_fields
+        b = raw[f * blk:(f + 1) * blk]
+        h = b[:256].view(np.int32)
+        m = b[256:256 + _lib.RDSE_BUCKETS * c.enc_w * 2].view(np.int16).reshape(_lib.RDSE_BUCKETS, c.enc_w)
+        lo, hi = int(h[0]), int(h[1])
+        rows = np.zeros((_lib.RDSE_BUCKETS, c.enc_w), np.int32)
+        rows[lo:hi + 1] = m[lo:hi + 1]
+        return dict(min_idx=lo, max_idx=hi, has_offset=int(h[2]), num_tries=int(h[3]),
+                    offset=float(h[4:6].view(np.float64)[0]), map=rows)
 
     def tm_segments(self, s: int) -> dict:
         """Live segments of stream s in canonical (cell, creation) order, the

@@ -102,6 +102,32 @@ class ScalarEncoder:
         return np.where(miss, -1, b)
 
 
+class RandomDistributedScalarEncoder:
+    """nupic.encoders.RandomDistributedScalarEncoder parameters -- the encoder
+    of the reference's model.yaml (ML/HTM/params/model.yaml:15-21).  Encoding
+    runs on the GPU (sp.hip rdse_encode_kernel, per-stream bucket maps and
+    offsets); bucket queries read the engine's HTM_OUT_BUCKETS output."""
+
+    MAX_BUCKETS = _lib.RDSE_BUCKETS
+
+    def __init__(self, resolution, w=21, n=400, name=None, offset=None, seed=42, verbosity=0, fieldname=None):
+        if w <= 0 or w % 2 == 0:
+            raise ValueError("w must be an odd positive integer")
+        if resolution <= 0:
+            raise ValueError("resolution must be a positive number")
+        if n <= 6 * w:
+            raise ValueError("n must be an int strictly greater than 6*w")
+        if offset is not None:
+            raise ValueError("RDSE offset: only None (the first value encoded) is supported")
+        self.w, self.n, self.resolution, self.seed = int(w), int(n), float(resolution), int(seed)
+        self.name = name if name is not None else "[%s]" % self.resolution
+        self.fieldname = fieldname if fieldname is not None else self.name
+        self.clipInput = True
+
+    def getWidth(self):
+        return self.n
+
+
 class MultiEncoder:
     """nupic.encoders.MultiEncoder: sub-encoders concatenated in sorted field
     name order (NetworkUtils.py:77-108)."""
@@ -118,11 +144,12 @@ class MultiEncoder:
         for key in sorted(fieldEncodings):
             spec = dict(fieldEncodings[key])
             kind = spec.pop("type", "ScalarEncoder")
-            if kind != "ScalarEncoder":
-                raise ValueError("encoder type %s is not supported (ScalarEncoder only)" % kind)
+            cls = {"ScalarEncoder": ScalarEncoder, "RandomDistributedScalarEncoder": RandomDistributedScalarEncoder}
+            if kind not in cls:
+                raise ValueError("encoder type %s is not supported (ScalarEncoder, RandomDistributedScalarEncoder)" % kind)
             fieldname = spec.pop("fieldname", key)
             name = spec.pop("name", key)
-            self.addEncoder(key, ScalarEncoder(name=name, fieldname=fieldname, **spec))
+            self.addEncoder(key, cls[kind](name=name, fieldname=fieldname, **spec))
 
     def fields(self):
         return [self.encoders[k] for k in sorted(self.encoders)]
@@ -304,11 +331,18 @@ def engine_config(sensor_enc: MultiEncoder | None, sp_params: dict, tm_params: d
         if len(fields) > 4:
             raise ValueError("at most 4 encoder fields (got %d)" % len(fields))
         for e in fields[1:]:
-            if (e.n, e.w, e.clipInput) != (e0.n, e0.w, e0.clipInput):
-                raise ValueError("all encoder fields must share n/w/clipInput")
-        over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_minval=e0.minval, enc_maxval=e0.maxval,
-                    enc_clip=int(e0.clipInput))
-        if any((e.minval, e.maxval) != (e0.minval, e0.maxval) for e in fields[1:]):
+            if (type(e), e.n, e.w, e.clipInput) != (type(e0), e0.n, e0.w, e0.clipInput):
+                raise ValueError("all encoder fields must share the encoder type and n/w/clipInput")
+        if isinstance(e0, RandomDistributedScalarEncoder):
+            if any((e.resolution, e.seed) != (e0.resolution, e0.seed) for e in fields[1:]):
+                raise ValueError("all RDSE fields must share resolution and seed")
+            over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_type=_lib.ENC_RDSE,
+                        rdse_resolution=e0.resolution, rdse_seed=e0.seed)
+        else:
+            over = dict(n_fields=len(fields), enc_n=e0.n, enc_w=e0.w, enc_minval=e0.minval, enc_maxval=e0.maxval,
+                        enc_clip=int(e0.clipInput))
+        if not isinstance(e0, RandomDistributedScalarEncoder) and \
+                any((e.minval, e.maxval) != (e0.minval, e0.maxval) for e in fields[1:]):
             # per-field ranges (e.g. cpu/mem % next to response times in ms)
             pad = [0.0] * (4 - len(fields))
             over["field_minval"] = tuple([float(e.minval) for e in fields] + pad)
@@ -446,7 +480,7 @@ class Network:
         enc = sensor.getSelf().encoder
         if enc is None:
             raise RuntimeError("sensor %r has no encoder" % sensor.name)
-        if isinstance(enc, ScalarEncoder):
+        if isinstance(enc, (ScalarEncoder, RandomDistributedScalarEncoder)):
             m = MultiEncoder()
             m.addEncoder(enc.name, enc)
             enc = m
@@ -491,7 +525,8 @@ class Network:
         from .classifier import SDRClassifier
         impl = r.getSelf()
         f0 = self._first_field()
-        nb = f0.n - f0.w + 1  # ScalarEncoder buckets (clipped, non-periodic)
+        # ScalarEncoder buckets (clipped, non-periodic); the RDSE's maxBuckets
+        nb = f0.MAX_BUCKETS if isinstance(f0, RandomDistributedScalarEncoder) else f0.n - f0.w + 1
         if impl.maxCategoryCount < nb:
             raise ValueError("maxCategoryCount %d < %d encoder buckets" % (impl.maxCategoryCount, nb))
         eng = self.levels[self._cls_level[r.name]].engine
@@ -511,7 +546,12 @@ class Network:
             learn, infer = r.modes["learningMode"], r.modes["inferenceMode"]
             f0 = f0 or self._first_field()
             pat = self.levels[k].engine.get_output("tm_output")
-            bucket = f0.bucket_indices(vals[:, 0]) if learn else None
+            if not learn:
+                bucket = None
+            elif isinstance(f0, RandomDistributedScalarEncoder):  # the GPU encoder's bucketIdxOut
+                bucket = self.levels[0].engine.get_output("buckets")[:, 0].cpu().numpy().astype(np.int64)
+            else:
+                bucket = f0.bucket_indices(vals[:, 0])
             prob, act = impl.classifier.compute(pat, bucket, vals[:, 0] if learn else None, learn=learn, infer=infer)
             impl.classifier.status()  # raises like NuPIC on an empty pattern (this record only)
             impl.recordNum += 1
@@ -569,7 +609,10 @@ class Network:
             if name == "actValueOut":
                 return vals[:, 0].astype(np.float64)
             if name == "bucketIdxOut":
-                return self._first_field().bucket_indices(vals[:, 0]).astype(np.float64)
+                f0 = self._first_field()
+                if isinstance(f0, RandomDistributedScalarEncoder):  # the GPU encoder's state
+                    return self.levels[0].engine.get_output("buckets")[:, 0].cpu().numpy().astype(np.float64)
+                return f0.bucket_indices(vals[:, 0]).astype(np.float64)
             if name == "sourceOut":
                 return vals.copy()
         elif region.type == SP:

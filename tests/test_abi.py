@@ -37,14 +37,15 @@ def test_struct_layouts_match_the_header(rt, tmp_path):
         '#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n'
         'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(htm_config), sizeof(htm_tm_header),'
         ' sizeof(htm_tm_update), offsetof(htm_config, tm_seed), offsetof(htm_tm_header, inf_pat_head),'
-        ' offsetof(htm_config, sdr_bits), offsetof(htm_config, sp_perm_rows));}\n' % HEADER)
+        ' offsetof(htm_config, sdr_bits), offsetof(htm_config, sp_perm_rows));'
+        'printf("%%zu %%zu\\n", offsetof(htm_config, enc_type), offsetof(htm_config, rdse_seed));}\n' % HEADER)
     exe = tmp_path / "probe"
     assert os.system(f"gcc {src} -o {exe}") == 0
     vals = [int(x) for x in os.popen(str(exe)).read().split()]
     L = rt._lib
     assert vals == [ctypes.sizeof(L.HtmConfig), ctypes.sizeof(L.TmHeader), ctypes.sizeof(L.TmUpdate),
                     L.HtmConfig.tm_seed.offset, L.TmHeader.inf_pat_head.offset, L.HtmConfig.sdr_bits.offset,
-                    L.HtmConfig.sp_perm_rows.offset]
+                    L.HtmConfig.sp_perm_rows.offset, L.HtmConfig.enc_type.offset, L.HtmConfig.rdse_seed.offset]
 
 
 def test_default_config_is_the_reference_model1(rt):
@@ -62,7 +63,7 @@ def test_default_config_is_the_reference_model1(rt):
 
 def test_abi_version_and_error_string(rt):
     L = rt._lib.lib()
-    assert L.htm_abi_version() == 3
+    assert L.htm_abi_version() == 4
     assert isinstance(L.htm_last_error(), bytes)
 
 
@@ -71,7 +72,20 @@ def test_invalid_config_rejected_without_gpu(rt):
     if torch.cuda.is_available():
         pytest.skip("CPU-only check")
     L = rt._lib.lib()
-    cfg = rt.default_config(sp_boost_strength=3.0)
-    h = ctypes.c_void_p()
-    code = L.htm_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h))
-    assert code != 0 and not h.value
+    for bad in (dict(sp_boost_strength=-1.0), dict(enc_type=1, enc_w=20), dict(enc_type=1, enc_n=100),
+                dict(enc_type=1, rdse_resolution=0.0), dict(enc_type=7)):
+        cfg = rt.default_config(**bad)
+        h = ctypes.c_void_p()
+        code = L.htm_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h))
+        assert code != 0 and not h.value, bad
+
+
+def test_model_yaml_config_is_the_reference_parameter_set(rt):
+    """ML/HTM/params/model.yaml:15-63 (RDSE resolution 0.88 / seed 1, SP seed
+    1956, potentialPct 0.85, inc 0.04, dec 0.005, boostStrength 3.0; TM 32 cells,
+    seed 1960, thresholds 16 / 12, pamLength 1)."""
+    c = rt._lib.model_yaml_config().as_dict()
+    assert (c["enc_type"], c["enc_n"], c["enc_w"], c["rdse_resolution"], c["rdse_seed"]) == (1, 400, 21, 0.88, 1)
+    assert (c["sp_seed"], c["sp_boost_strength"], c["tm_cells_per_col"], c["tm_seed"]) == (1956, 3.0, 32, 1960)
+    assert abs(c["sp_potential_pct"] - 0.85) < 1e-7 and abs(c["sp_perm_active_inc"] - 0.04) < 1e-8
+    assert (c["tm_activation_threshold"], c["tm_min_threshold"], c["tm_pam_length"]) == (16, 12, 1)
