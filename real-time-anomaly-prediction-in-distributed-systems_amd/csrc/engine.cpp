@@ -1321,6 +1321,7 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
         const Region& src = model->regions[id];
         const Region& dst = e->regions[id];
         if (id == HTM_ST_SP_PERM_CKPT) continue;
+        if (src.per_stream == 0 && dst.per_stream == 0) continue;  // (no RDSE state: a ScalarEncoder model)
         if (id == HTM_ST_SP_PERM && model->dc.sp_paged) {
             std::vector<uint8_t> buf(src.per_stream);
             r = htm_export_state(const_cast<htm_engine*>(model), id, model_stream, 1, buf.data(), buf.size());

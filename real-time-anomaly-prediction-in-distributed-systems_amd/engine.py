@@ -213,6 +213,8 @@ class HTMEngine:
         per = self.state_bytes(region)
         if region == "sp_perm_ckpt" and (per == 0 or data.nbytes == 0):
             return  # SP checkpoints exist only in paged engines: none given or none held, keep the stream's own
+        if per == 0:
+            return  # a region this engine does not hold (e.g. RDSE state of a ScalarEncoder engine)
         n = data.nbytes // per
         check(self._L.htm_import_state(self.h, ST[region], s0, n, data.ctypes.data_as(ctypes.c_void_p), data.nbytes))
 
