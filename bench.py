@@ -129,6 +129,97 @@ def cpu_baseline(trace, train_vals, n_total, target_s=12.0):
                                      "source": "CSC 724 Final Project Report p.8 (SURVEY.md §6)"})
 
 
+def learn_on_bytes(eng, S, seg_live):
+    """Unique algorithmic bytes per stream-step of a learning step (SURVEY.md
+    §8(d)'s learning terms, each byte counted once per step however often the
+    kernel re-reads it -- a lower bound, write traffic of new segments and
+    weak-column bumps excluded): SP -- the active input rows of the
+    input-major connected map, the winners' potential permanences read and
+    written and their potential-mask rows, both duty-cycle arrays read and
+    written; TM -- every live segment's meta, synapse sources, connected mask
+    and dutyCycle record read once, the winners' segment permanences read and
+    written (one segment per active column), the seven cell bitmaps read and
+    written, the pattern history."""
+    c = eng.config
+    nw, pw = c.sp_columns // 32, (c.n_fields * c.enc_n + 31) // 32
+    n_pot = int(round(c.n_fields * c.enc_n * c.sp_potential_pct))
+    sp = c.n_fields * c.enc_w * nw * 4 + c.sp_num_active * (n_pot * 4 * 2 + pw * 4) + 2 * c.sp_columns * 4 * 2
+    cw = c.sp_columns * c.tm_cells_per_col // 32
+    tm = seg_live / S * (4 + 64 + 4 + 12) + c.sp_num_active * 128 * 2 + 7 * cw * 4 * 2 + 2 * 16 * 64 * 2
+    return sp + tm
+
+
+def bench_learn_on(args, rt, trace, world, rank, local, pmc_summary=None, pmc_note=None):
+    """The "learn on" half of BASELINE.json's metric (configs[2], SURVEY.md
+    §8(d) config 3): 65,536 fresh Model-1 streams per GPU (seeds 2045 + the
+    global stream index), SP+TM learning on, paged SP permanences (800 rows per
+    stream), `learn_steps` lockstep htm_step calls timed after `learn_warmup`
+    untimed ones, the barrier / max-over-ranks contract of the headline.  Its
+    roofline counts unique bytes (learn_on_bytes)."""
+    import torch
+    S = args.learn_streams
+    n_total = S * world
+    import _pkg
+    s0, s1 = _pkg.load().fleet.shard_range(n_total, world, rank)
+    dev = f"cuda:{local}"
+    cfg = rt.default_config(seg_capacity=10240, upd_capacity=512, seed_stride=1, sp_seed=2045 + s0, tm_seed=2045 + s0,
+                            sp_perm_rows=800)
+    t0 = time.time()
+    eng = rt.HTMEngine(S, config=cfg, device=local)
+    torch.cuda.synchronize()
+    init_s = time.time() - t0
+    eng.set_learning(True, True)
+    W, K = args.learn_warmup, args.learn_steps
+    vals = torch.tensor(make_inputs(n_total, s0, s1, 0, W + K, trace), device=dev)
+    scores = torch.empty((W + K, S), dtype=torch.float32, device=dev)
+    for k in range(W):
+        eng.step(vals[k], out=scores[k])
+    torch.cuda.synchronize()
+    c0 = eng.counters()
+    eng.profile(True)
+    dt, _ = timed_replay(eng, vals, scores, W, K, "step", 1, None, None, rank, world, dev)
+    prof = eng.profile_read()
+    eng.profile(False)
+    c1 = eng.counters()
+    if c1["error"]:
+        raise RuntimeError(f"learn-on engine overflow flags {c1['error']}")
+    seg_live = (c0["seg_live"] + c1["seg_live"]) / 2
+    per_ss = learn_on_bytes(eng, S, seg_live)
+    launches = prof["launches"]
+    avg_ms = prof["tm_ms"] / launches
+    per_launch = per_ss * S
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9
+    traffic, tsrc = None, pmc_note
+    if pmc_summary:
+        k = pmc_kernel(pmc_summary, "htm_run_kernel<true>")
+        if k:
+            traffic = int(k["hbm_bytes_per_dispatch"])
+            tsrc = f"rocprofv3 --pmc passes of the learn-on leg ({pmc_summary}): {k.get('formula', '')}"
+    rec = {"value": round(n_total * K / dt, 1), "unit": "stream-steps/s", "steps": K, "warmup": W,
+           "ms_per_step": round(dt / K * 1e3, 4),
+           "config": {"workload": "config3: fresh Model-1 streams (seed 2045+s), SP+TM learning on, lockstep htm_step",
+                      "streams_per_gpu": S, "total_streams": n_total, "sp_perm_rows": 800,
+                      "sp_perm_rows_used_per_stream": round(eng.sp_perm_rows_used() / S, 1),
+                      "live_segments_per_stream": round(c1["seg_live"] / S, 1), "init_s": round(init_s, 2),
+                      "device_gb": round(eng.device_bytes() / 1e9, 1)},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                        "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
+                        "traffic_source": tsrc, "kernel": "htm_run_kernel<true>", "avg_launch_ms": round(avg_ms, 4),
+                        "bytes_per_launch": int(per_launch), "bytes_per_stream_step": int(per_ss),
+                        "bytes_rule": "unique bytes (bench.learn_on_bytes, SURVEY.md 8(d) learning terms)"},
+           "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks", "lrn_phase2", "lrn_backtracks"]}}
+    eng.close()
+    return rec
+
+
+def pmc_kernel(path, base):
+    pm = json.load(open(path))
+    ks = [v for n, v in pm.get("kernels", {}).items()
+          if n.split("(")[0].replace("void ", "").strip() == base and "hbm_bytes_per_dispatch" in v]
+    return ks[0] if ks else None
+
+
 def bench_config5(args, rt, d, world, rank, local):
     """Config 5 (BASELINE.json configs[4]): the Models 2/3 encoder -- cpu + mem
     ScalarEncoders (ML/HTM/NetworkUtils.py:89-107, 1000 input bits) -- into a
@@ -291,6 +382,15 @@ def main():
                          "(same gpurun call): fills roofline.traffic")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the counter passes bench.py runs itself (N=1) to fill roofline.traffic")
+    ap.add_argument("--no-learn-on", action="store_true",
+                    help="config 2: skip the learn_on sub-record (config 3's learning streams, BASELINE's 'learn on')")
+    ap.add_argument("--learn-streams", type=int, default=65536, help="learn_on: streams per GPU")
+    ap.add_argument("--learn-steps", type=int, default=32, help="learn_on: timed lockstep steps")
+    ap.add_argument("--learn-warmup", type=int, default=8, help="learn_on: untimed steps")
+    ap.add_argument("--pmc-summary-learn", default=None, help="counter summary of the learn_on leg (see --pmc-summary)")
+    ap.add_argument("--shape", choices=["model1", "yaml"], default="model1",
+                    help="model1 (default): the reference's Model-1 parameters (12 cells/column); yaml: the "
+                         "reference's model.yaml set (RDSE, boostStrength 3, 32 cells/column; configs 2 and 4)")
     args = ap.parse_args()
     c3, c4, c5 = args.config == 3, args.config == 4, args.config == 5
     if c5:
@@ -307,20 +407,23 @@ def main():
     if args.sp_perm_rows is None:
         args.sp_perm_rows = 800 if c3 else 0
     if args.seg_capacity is None:
-        args.seg_capacity = 10240 if c3 else 72 * 1024
+        args.seg_capacity = 10240 if c3 else (1 << 17) if args.shape == "yaml" else 72 * 1024
     if args.chunk is None:
         args.chunk = 64 if c4 else 256 if (c3 or c5) else args.steps
     if args.other_steps is None:
         args.other_steps = 0 if c3 else 64 if c4 else 2324
     if c4:
         args.chunk = min(args.chunk, int(os.environ.get("HTM_C4_MAX_CHUNK", "64")))
-    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.pmc_summary and not args.no_pmc and not c5
+    learn_on = args.config == 2 and not args.no_learn_on and args.shape == "model1"
+    pmc_note = pmc_note_learn = None
+    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_pmc and not c5
             and not os.environ.get("HTM_BENCH_PMC_CHILD")):
         # before this process touches the GPU: the HBM counter passes, each a
         # short run of this same command under rocprofv3 in a child process
-        args.pmc_summary, pmc_note = self_pmc_passes(args)
-    else:
-        pmc_note = None
+        if not args.pmc_summary:
+            args.pmc_summary, pmc_note = self_pmc_passes(args)
+        if learn_on and not args.pmc_summary_learn:
+            args.pmc_summary_learn, pmc_note_learn = self_pmc_passes(args, learn_leg=True)
 
     import torch
     import torch.distributed as dist
@@ -343,6 +446,8 @@ def main():
     S = args.streams
     n_total = S * world
     s0, s1 = rt.fleet.shard_range(n_total, world, rank)
+    # the reference's model.yaml parameter set (RDSE, boosting, 32 cells/column) or Model 1
+    shape = dict(rt._lib.MODEL_YAML) if args.shape == "yaml" else {}
     if c3:
         # fresh per-stream init (seeds 2045 + global stream index), learning on
         cfg = rt.default_config(seg_capacity=args.seg_capacity, upd_capacity=512, seed_stride=1,
@@ -354,11 +459,13 @@ def main():
         eng.set_learning(True, True)
     elif c4:
         # one model trained on the GPU (2184 Model-1 records), shared by every stream
-        model, train_s, hdr, model_dist = trained_engine(rt, 1, args.seg_capacity, local, train_vals, world=world)
+        model, train_s, hdr, model_dist = trained_engine(rt, 1, args.seg_capacity, local, train_vals, world=world,
+                                                         **shape)
         eng = rt.HTMEngine.fleet(model, S, q_capacity=4096)
         model.close()
     else:
-        eng, train_s, hdr, model_dist = trained_engine(rt, S, args.seg_capacity, local, train_vals, world=world)
+        eng, train_s, hdr, model_dist = trained_engine(rt, S, args.seg_capacity, local, train_vals, world=world,
+                                                       **shape)
         eng.set_learning(False, False)
     if not c3:
         eng.set_run_chunk(args.chunk)  # one fused launch per htm_run call
@@ -408,19 +515,17 @@ def main():
                              rank, world, dev)
         other = {"mode": omode, "value": round(n_total * args.other_steps / dl, 1), "steps": args.other_steps,
                  "ms_per_step": round(dl / args.other_steps * 1e3, 4)}
+    shape_name = ("model.yaml-shape (RDSE resolution 0.88, SP boostStrength 3.0, 2048 columns, 32-cell "
+                  "BacktrackingTM; ML/HTM/params/model.yaml)" if args.shape == "yaml" else
+                  "Model-1 (2048-col SP, 12-cell BacktrackingTM)")
     roof = None
-    sp_bytes = 0
-    if c3:
-        # SP learning per stream-step (not counted on the device): the 21 active
-        # input rows of the connected map, 40 active columns' potential
-        # permanences read+written, potential-mask rows, duty cycles read+written
-        # (SURVEY.md §8(d), weak-column bumps W excluded: a lower bound)
-        sp_bytes = 21 * 256 + 40 * 400 * 4 * 2 + 40 * 64 + 2 * 2048 * 4 * 2
     if prof is not None and prof["tm_ms"] > 0:
-        tm_bytes = c1["tm_bytes"] - c0["tm_bytes"] + sp_bytes * S * args.steps
         launches = prof["launches"]
         avg_ms = prof["tm_ms"] / launches
-        per_launch = tm_bytes / launches
+        if c3:  # learning: unique bytes (the in-kernel count charges every pool re-scan)
+            per_launch = learn_on_bytes(eng, S, (c0["seg_live"] + c1["seg_live"]) / 2) * S * prof["steps"] / launches
+        else:   # frozen inference: the kernel's own count of the index blocks and state it moves
+            per_launch = (c1["tm_bytes"] - c0["tm_bytes"]) / launches
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
         traffic, tsrc = None, pmc_note
         if args.pmc_summary:
@@ -449,14 +554,15 @@ def main():
         "data": "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config %d)"
                 % args.config,
         "config": {"workload": ("config3: fresh Model-1 streams (seed 2045+s), SP+TM learning on" if c3 else
-                                "config4 fleet: streams sharing one frozen GPU-trained Model-1 SP+TM, "
-                                "per-stream TM state, learn off" if c4 else
-                                "config2: Model-1 streams (2048-col SP, 12-cell BacktrackingTM), SP+TM learn off, "
-                                "from the GPU-trained Model-1 state"),
+                                "config4 fleet: streams sharing one frozen GPU-trained %s SP+TM, "
+                                "per-stream TM state, learn off" % shape_name if c4 else
+                                "config2: %s streams, SP+TM learn off, from the GPU-trained state" % shape_name),
+                   "shape": args.shape,
                    "mode": ("lockstep: one htm_step (one fused launch) per step, every stream advances one "
                             "network.run(1) per step" if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
-                   "streams_per_gpu": S, "total_streams": n_total, "columns": 2048, "cells_per_column": 12,
+                   "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
+                   "cells_per_column": eng.cells_per_column,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
                    "segments_after": int(c1["seg_live"] // S) if c3 else None,
                    "sp_perm_rows": ({"per_stream": args.sp_perm_rows, "used_per_stream": round(eng.sp_perm_rows_used() / S, 1),
@@ -468,11 +574,13 @@ def main():
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
         ("run_mode" if args.mode == "step" else "lockstep"): other,
     }
-    if rank == 0 and world == 1 and not args.no_cpu and not c3 and not c4:
+    if rank == 0 and world == 1 and not args.no_cpu and not c3 and not c4 and args.shape == "model1":
         out["cpu_baseline"] = cpu_baseline(trace, train_vals, n_total)
+    eng.close()
+    if learn_on:
+        out["learn_on"] = bench_learn_on(args, rt, trace, world, rank, local, args.pmc_summary_learn, pmc_note_learn)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -486,10 +594,11 @@ PMC_PASSES = {
 }
 
 
-def self_pmc_passes(args, steps=128):
+def self_pmc_passes(args, steps=128, learn_leg=False):
     """Run this benchmark's workload (same config/streams, `steps` timed steps,
     the same launch shape as the timed region) under rocprofv3 once per
-    counter pass and summarise them (tools/pmc_summary.py).  Returns
+    counter pass and summarise them (tools/pmc_summary.py); learn_leg: the
+    learn_on leg's workload (config 3 at --learn-streams, lockstep).  Returns
     (summary path, note); (None, reason) when the passes cannot run."""
     import shutil
     import subprocess
@@ -499,12 +608,18 @@ def self_pmc_passes(args, steps=128):
     if not prof:
         return None, "rocprofv3 not found: traffic not measured"
     out = tempfile.mkdtemp(prefix="htm_pmc_", dir="/tmp")
-    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
-             "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode]
-    for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows"):
-        v = getattr(args, k)
-        if v is not None:
-            child += ["--" + k.replace("_", "-"), str(v)]
+    if learn_leg:
+        child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "3", "--steps", "16", "--warmup",
+                 str(args.learn_warmup), "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", "step",
+                 "--streams", str(args.learn_streams)]
+    else:
+        child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
+                 "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode,
+                 "--no-learn-on", "--shape", args.shape]
+        for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows"):
+            v = getattr(args, k)
+            if v is not None:
+                child += ["--" + k.replace("_", "-"), str(v)]
     env = dict(os.environ, TMPDIR="/tmp", HTM_BENCH_PMC_CHILD="1")
     for name, counters in PMC_PASSES.items():
         t0 = time.time()

@@ -8,13 +8,19 @@ MAX_LEAD_TIME = 50          # ModelTesting.py:31
 SLO_RESPONSE_TIME = 70      # ModelTesting.py:32
 
 
-def evaluate(windows, means, violations, threshold, max_lead=MAX_LEAD_TIME):
+def evaluate(windows, means, violations, threshold, max_lead=MAX_LEAD_TIME, cut=None, labels=None):
     """windows[r] = the 1+7 anomaly scores of record r (ModelTesting.py:66-72).
-    Returns (tp, fp, tn, fn, avg_lead or None) as getModelStats prints them."""
+    Returns (tp, fp, tn, fn, avg_lead or None) as getModelStats prints them.
+    For oracle/label_rule_search.py only: `cut` (default max_lead) is the tail
+    getModelStats leaves out, `labels` (0/1 per record) replaces :57-60's rule."""
+    cut = max_lead if cut is None else cut
     pl = []
     for r0, win in enumerate(windows):
         rcount = r0 + 1                                        # :62
-        violation = 1 if (violations[r0] > 0 or means[r0] >= SLO_RESPONSE_TIME) else 0   # :57-60
+        if labels is not None:
+            violation = int(labels[r0])
+        else:
+            violation = 1 if (violations[r0] > 0 or means[r0] >= SLO_RESPONSE_TIME) else 0   # :57-60
         n_over = sum(1 for a in win if float(a) > threshold)   # :75-77 (float32 vs double)
         if n_over > 0 and rcount > 1:                          # :81
             pl.append([-1, 'A', rcount, 'TP', 0])
@@ -49,7 +55,7 @@ def evaluate(windows, means, violations, threshold, max_lead=MAX_LEAD_TIME):
                         item[0] = 0
     tp = fp = tn = fn = 0
     lead = 0.0
-    for item in pl[:-max_lead]:                                # getModelStats :148-171
+    for item in pl[:-cut]:                                     # getModelStats :148-171
         if item[3] == 'TP':
             tp += 1
             lead += item[4]

@@ -52,13 +52,14 @@ struct Region {
 };
 
 // lockstep launches between two flushes of the deferred log, and the grid of
-// a flush that runs beside the steps: a few workgroups fill the gaps the
+// a flush that runs beside the steps: a part of the chip fills the gaps the
 // steps' tails leave; a full-width flush beside them takes the slots the next
-// step's workgroups need (measured on config 2, profiles/r03_flush: 1,024 /
-// every 8 0.319 ms per step, 64 / 8 0.251, 128 / 16 0.249, the round-2
-// full-width flush on the step stream every 32 steps 0.263)
-#define FLUSH_EVERY 16
-#define FLUSH_WG 128
+// step's workgroups need (measured on config 2, 256-step regions ending with
+// htm_flush, profiles/r03_flush: 1,024 workgroups every 8 steps 0.319 ms per
+// step, 128 / 16 0.244, 256 / 8 0.243, the round-2 full-width flush on the
+// step stream every 32 steps 0.246; 20-step regions 0.278 / 0.258 / 0.269)
+#define FLUSH_EVERY 8
+#define FLUSH_WG 256
 
 struct htm_engine {
     htm_config cfg;

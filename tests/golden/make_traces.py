@@ -25,7 +25,8 @@ def load(path):
         return np.nan if v in (None, "None", "null") else float(v)
 
     return (np.array([f(r["cpu"]) for r in rows]), np.array([f(r["mem"]) for r in rows]),
-            np.array([int(r["mean"]) for r in rows]), np.array([int(r["violations"]) for r in rows]))
+            np.array([int(r["mean"]) for r in rows]), np.array([int(r["violations"]) for r in rows]),
+            np.array([int(r["max"]) for r in rows]), np.array([int(r["count"]) for r in rows]))
 
 
 def main():
@@ -34,7 +35,9 @@ def main():
     tr = load(os.path.join(REF, "TrainingData.txt"))
     te = load(os.path.join(REF, "TestingData.txt"))
     np.savez_compressed(OUT, train_cpu=tr[0], train_mem=tr[1], train_mean=tr[2], train_violations=tr[3],
-                        test_cpu=te[0], test_mem=te[1], test_mean=te[2], test_violations=te[3])
+                        train_max=tr[4], train_count=tr[5],
+                        test_cpu=te[0], test_mem=te[1], test_mean=te[2], test_violations=te[3],
+                        test_max=te[4], test_count=te[5])
     print("wrote", OUT, len(tr[0]), len(te[0]))
     write_sweep()
 
