@@ -27,6 +27,13 @@
 #define FX_DEPTH 4                 // frozen index: out-list blocks in flight per thread
 #endif
 #define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
+// index of the block-list offset of (window w, cell x); FX_CELL_MAJOR (A/B
+// builds only) restores the round-2 [cell][window] order
+#ifdef FX_CELL_MAJOR
+#define FX_LIST(c, w, x) ((size_t)(x) * (c).fx_nwin + (size_t)(w))
+#else
+#define FX_LIST(c, w, x) ((size_t)(w) * (c).ncells + (size_t)(x))
+#endif
 #define FX_MAXPER ((HTM_MAXACT * HTM_MAXK + TM_NT - 1) / TM_NT)  // active cells per thread
 
 // Derived, immutable engine constants (kernel argument).
@@ -145,10 +152,12 @@ struct TmBufs {
     // are numbered by RANK in NuPIC's (cell, creation) order -- the order
     // _inferPhase2 sums confidences in -- so segments that qualify, found by a
     // sweep over rank-ordered counters, come out already in summation order.
-    // For stream s, cell x and counter window w (a range of fx_win ranks), the
+    // For stream s, counter window w (a range of fx_win ranks) and cell x, the
     // window-relative ranks (u16) of the segments with a synapse from x fill
-    // the 16-byte blocks fx_ent[fx_base[s] + fx_off[s][x][w] .. fx_off[s][x][w+1]),
-    // padded with 0xFFFF, so one uint4 load delivers 8 entries of one list
+    // the 16-byte blocks fx_ent[fx_base[s] + fx_off[s][w][x] .. fx_off[s][w][x+1]),
+    // padded with 0xFFFF, so one uint4 load delivers 8 entries of one list.
+    // Window-major: within a window the lists of consecutive cells are
+    // adjacent, so a bursting column's cells stream as one contiguous run
     // The same block pool also holds, per cell, the list of predictive-
     // capable segment ids (pid: live segments with >= activationThreshold
     // connected synapses, numbered densely in slot order) that the cell
@@ -157,7 +166,7 @@ struct TmBufs {
     // needs of a qualifying segment: its cell and the dutyCycle value it
     // reads while learning is off (the iteration counter is frozen).
     uint64_t* fx_base;      // [S] first block of the stream
-    uint32_t* fx_off;       // [S][fx_noff]: [cell][window] lists, then [cell] pid lists, then the end
+    uint32_t* fx_off;       // [S][fx_noff]: [window][cell] lists, then [cell] pid lists, then the end
     uint4* fx_ent;          // [total blocks] 8 x u16 entries each
     uint2* fx_rec;          // [S][seg_cap] by rank: {cell | FX_FRESH, dutyCycle bits}
     uint32_t* fx_rslot;     // [S][seg_cap] pool slot of each rank

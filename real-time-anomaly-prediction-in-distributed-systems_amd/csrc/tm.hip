@@ -208,7 +208,7 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
         const uint32_t m = meta[slot];
         const uint32_t nsyn = meta_nsyn(m), w = r / (uint32_t)c.fx_win;
         for (uint32_t j = 0; j < nsyn; j++)
-            atomicAdd(&off[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+            atomicAdd(&off[FX_LIST(c, w, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
         const uint32_t cm = conn[slot] & (nsyn >= 32 ? ~0u : ((1u << nsyn) - 1u));
         uint32_t p = ~0u;
         if (__popc(cm) >= (uint32_t)c.act_thr) {
@@ -301,7 +301,7 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
         const uint32_t m = meta[slot];
         const uint32_t nsyn = meta_nsyn(m), w = r / W;
         for (uint32_t j = 0; j < nsyn; j++) {
-            uint32_t pos = atomicAdd(&cur[(size_t)src[(size_t)slot * HTM_MAXSYN + j] * c.fx_nwin + w], 1u);
+            uint32_t pos = atomicAdd(&cur[FX_LIST(c, w, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
             ent[pos] = (uint16_t)(r - w * W);
         }
         // FX_FRESH: the record already holds what a frozen dutyCycle() stores

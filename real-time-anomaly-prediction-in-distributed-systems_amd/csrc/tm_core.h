@@ -590,7 +590,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
     constexpr uint32_t FX_PF = 2;
     uint32_t olo[FX_PF], ohi[FX_PF];
     auto off_idx = [&](int w, uint32_t k) {
-        return w < 0 ? (size_t)c.ncells * nwin + cells[k] : (size_t)cells[k] * nwin + (uint32_t)w;
+        return w < 0 ? (size_t)c.ncells * nwin + cells[k] : FX_LIST(c, (uint32_t)w, cells[k]);
     };
     auto load_offsets = [&](int w) {
 #pragma unroll
