@@ -103,11 +103,13 @@ struct htm_engine {
     int32_t flush_wg = FLUSH_WG;      // grid of a flush beside the steps
     int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
+    bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
 };
 
 
 static int flush_deferred(htm_engine* e, hipStream_t st);
 static int flush_sync(htm_engine* e);
+static int densify_conf(htm_engine* e, hipStream_t st);
 
 extern "C" {
 
@@ -398,6 +400,7 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.scr_q2, uint32_t, std::max(S * (size_t)d.q_cap, cap));
     ALLOC(e->tm.prev_pred, uint8_t, S * d.ncol);
     ALLOC(e->tm.colnz, uint32_t, S * ((size_t)d.nw + 1));
+    ALLOC(e->tm.colval, float, S * d.ncol);
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
@@ -838,6 +841,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
+    e->conf_packed = true;
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
     if (defer && ++e->defer_steps >= std::min(e->flush_every ? e->flush_every : FLUSH_EVERY, e->dc.fx_dcap / 2)) {
         int r = flush_async(e, st);  // beside the next steps
@@ -869,6 +873,7 @@ static int step_unfused(htm_engine* e, const double* d_values, const uint32_t* d
     tb.fx_dlog = nullptr;  // (deferred duty writes: fused lockstep launches only)
     if (launch_tm_step(e->dc, tb, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
         return htm_fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
+    e->conf_packed = true;
     if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
 }
@@ -1026,8 +1031,11 @@ __global__ void out_kernel(DevCfg c, SpBufs sp, TmBufs tm, int which, uint8_t* d
 
 __global__ void prev_pred_kernel(DevCfg c, TmBufs tm) {
     const int s = blockIdx.x;
+    const uint32_t* nz = tm.colnz + (size_t)s * (c.nw + 1);
+    const bool packed = nz[c.nw] == 1u;  // the bitmap is current (else the dense copy is)
     for (int i = threadIdx.x; i < c.ncol; i += blockDim.x)
-        tm.prev_pred[(size_t)s * c.ncol + i] = tm.colconf[(size_t)s * c.ncol + i] != 0.0f ? 1 : 0;
+        tm.prev_pred[(size_t)s * c.ncol + i] =
+            packed ? (uint8_t)((nz[i >> 5] >> (i & 31)) & 1u) : (tm.colconf[(size_t)s * c.ncol + i] != 0.0f ? 1 : 0);
 }
 
 int launch_prev_pred(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
@@ -1081,6 +1089,7 @@ int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void
             return HTM_OK;
         }
         case HTM_OUT_COL_CONFIDENCE:
+            if (int r = densify_conf(e, st)) return r;
             HIP_TRY(hipMemcpyAsync(d_dst, e->tm.colconf, per * e->n, hipMemcpyDeviceToDevice, st));
             return HTM_OK;
         case HTM_OUT_SP_OVERLAPS:
@@ -1195,6 +1204,7 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
     const Region& r = e->regions[region];
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "export buffer too small");
     if (int rf = flush_sync(e)) return rf;
+    if (int rd = densify_conf(e, nullptr)) return rd;
     HIP_TRY(hipDeviceSynchronize());
     if (r.per_stream == 0) return HTM_OK;
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_export(e, s0, n, h_dst, nullptr);
@@ -1202,10 +1212,44 @@ int htm_export_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, void*
     return HTM_OK;
 }
 
-// The kernels write colConfidence back sparsely against a per-stream bitmap
-// of its nonzero columns (TmBufs::colnz); any host-side change of the TM
-// state marks the bitmaps stale, so the next write-back is dense.
+// The kernels write colConfidence back packed (TmBufs::colnz bitmap +
+// colval values); the dense per-stream copy (HTM_ST_TM_COLCONF, colconf) is
+// rebuilt from it before the host reads or replaces any state: one workgroup
+// per stream whose packed form is current.
+__global__ void conf_densify_kernel(DevCfg c, TmBufs b) {
+    const int s = blockIdx.x;
+    const uint32_t* nz = b.colnz + (size_t)s * (c.nw + 1);
+    if (nz[c.nw] != 1u) return;  // the dense copy is current
+    __shared__ uint32_t woff[HTM_MAXNW];
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < c.nw; w++) {
+            woff[w] = run;
+            run += (uint32_t)__popc(nz[w]);
+        }
+    }
+    __syncthreads();
+    const float* v = b.colval + (size_t)s * c.ncol;
+    float* d = b.colconf + (size_t)s * c.ncol;
+    for (int col = threadIdx.x; col < c.ncol; col += blockDim.x) {
+        const uint32_t w = nz[col >> 5];
+        d[col] = ((w >> (col & 31)) & 1u) ? v[woff[col >> 5] + __popc(w & ((1u << (col & 31)) - 1u))] : 0.0f;
+    }
+}
+
+static int densify_conf(htm_engine* e, hipStream_t st) {
+    if (!e->conf_packed) return HTM_OK;
+    hipLaunchKernelGGL(conf_densify_kernel, dim3(e->n), dim3(256), 0, st, e->dc, e->tm);
+    HIP_TRY(hipGetLastError());
+    e->conf_packed = false;
+    return HTM_OK;
+}
+
+// Any host-side change of the TM state: the dense colConfidence becomes the
+// current copy (densified first) and the packed form is marked stale, so the
+// next step starts from the dense copy and writes back in full.
 static int invalidate_colnz(htm_engine* e, void* stream) {
+    if (int r = densify_conf(e, (hipStream_t)stream)) return r;
     const size_t bytes = (size_t)e->n * ((size_t)e->dc.nw + 1) * 4;
     if (hipMemsetAsync(e->tm.colnz, 0, bytes, (hipStream_t)stream) != hipSuccess)
         return htm_fail(HTM_E_HIP, "colnz reset: %s", hipGetErrorString(hipGetLastError()));
@@ -1224,6 +1268,7 @@ static int import_region(htm_engine* e, int32_t region, int32_t s0, int32_t n, c
     if (bytes < r.per_stream * n) return htm_fail(HTM_E_INVALID, "import buffer too small");
     if (r.per_stream == 0) return HTM_OK;  // (a region this engine does not have, e.g. RDSE state)
     if (int rf = flush_sync(e)) return rf;
+    if (int rd = densify_conf(e, nullptr)) return rd;  // (before the dense copy may be overwritten)
     HIP_TRY(hipDeviceSynchronize());
     if (region == HTM_ST_SP_PERM && e->dc.sp_paged) return paged_perm_import(e, s0, n, h_src, nullptr, 0);
     if (rebase && e->dc.sp_paged && (region == HTM_ST_SP_PERM_CKPT || region == HTM_ST_SP_POTMASK))
@@ -1274,6 +1319,7 @@ int htm_replicate_stream(htm_engine* e, int32_t src, void* stream) {
     if (!e || src < 0 || src >= e->n) return htm_fail(HTM_E_INVALID, "bad source stream");
     hipStream_t st = (hipStream_t)stream;
     if (int rf = flush_sync(e)) return rf;
+    if (int rd = densify_conf(e, st)) return rd;
     for (int id = 1; id <= HTM_ST_COUNT; id++) {
         const Region& r = e->regions[id];
         if (!r.base || !r.per_stream) continue;
@@ -1311,6 +1357,7 @@ int htm_create_fleet(const htm_engine* model, int32_t model_stream, int32_t n_st
     *out = nullptr;
     HIP_TRY(hipSetDevice(model->device));
     if (int rf = flush_sync(const_cast<htm_engine*>(model))) return rf;
+    if (int rd = densify_conf(const_cast<htm_engine*>(model), nullptr)) return rd;
     HIP_TRY(hipDeviceSynchronize());
     htm_engine* e = nullptr;
     htm_config fcfg = model->cfg;

@@ -146,7 +146,8 @@ struct TmBufs {
     uint32_t* scr_q;        // [S][q_cap]: qualifying segment keys
     uint32_t* scr_q2;       // [S][q_cap] (>= seg_cap entries): bucket-sorted keys / index-build pid map
     uint8_t* prev_pred;     // [S][ncol] nonzero(colConf(t-1)) captured before compute
-    uint32_t* colnz;        // [S][nw + 1]: nonzero columns of colconf, word nw = 1 when valid
+    uint32_t* colnz;        // [S][nw + 1]: nonzero columns of colconf, word nw = 1 when the packed form is current
+    float* colval;          // [S][ncol]: packed colConfidence, the nonzero columns' values in column order
     uint32_t* scr_cur;      // [S][ncells*fx_nwin] frozen-index fill cursors
     // frozen forward index (valid while TM learning is off).  Live segments
     // are numbered by RANK in NuPIC's (cell, creation) order -- the order

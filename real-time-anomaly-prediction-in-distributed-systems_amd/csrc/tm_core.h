@@ -2082,12 +2082,15 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
 // infActiveState words that differ from HBM (the old words are loaded first,
 // their latency hidden behind the colConfidence bitmap), infPredictedState
 // words that differ from infP(t-1) (on the first step of a run the LDS copy
-// is what HBM holds), and colConfidence sparsely: gnz[0..nw) is the
-// nonzero-column bitmap of the dense HBM copy, gnz[nw] == 1 says it is valid
-// (the host clears it whenever it changes the state), so only the columns
-// nonzero before or now are written.  Uses t.flags (free after the TM step).
-// Returns the bytes this thread moved.  Contains barriers.
-__device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint32_t* gbm, float* gconf,
+// is what HBM holds), and colConfidence PACKED: gnz[0..nw) is the bitmap of
+// its nonzero columns and gval[0..n) their values in ascending column order
+// (one contiguous run of stores, not a scatter over the dense columns);
+// gnz[nw] == 1 says the packed form is current (the host densifies it into
+// TmBufs::colconf before it reads or replaces the state, then clears the
+// flag, and the next step starts from the dense copy).  Uses t.flags and the
+// head of t.U (free after the TM step).  Returns the bytes this thread moved.
+// Contains barriers.
+__device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint32_t* gbm, float* gval,
                                                          uint32_t* gnz) {
     const DevCfg& c = t.c;
     constexpr int PER = 4;  // old infA words prefetched per thread (all of them up to 32,768 cells)
@@ -2105,13 +2108,7 @@ __device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint
     }
     const bool valid = gnz[c.nw] == 1u;
     uint32_t* nzb = t.flags;  // the new bitmap
-    uint32_t* ozb = t.U;      // the old one (the union is free after the step)
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        if (w < c.nw) ozb[w] = oldnz[j];
-    }
+    uint32_t* woff = t.U;     // packed position of each bitmap word's first column
     // nonzero-column bitmap of the LDS colConfidence (ballots over 64 columns)
     for (int col0 = wave_id() * 64; col0 < c.ncol; col0 += TM_NT) {
         const int col = col0 + lane_id();
@@ -2122,12 +2119,17 @@ __device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint
         }
     }
     __syncthreads();
+    // word offsets: exclusive prefix of the words' popcounts (nw <= 128 < TM_NT)
+    uint32_t tot;
+    const uint32_t mine = threadIdx.x < (uint32_t)c.nw ? (uint32_t)__popc(nzb[threadIdx.x]) : 0u;
+    const uint32_t off = wg_excl_scan(t.sh, mine, &tot);
+    if (threadIdx.x < (uint32_t)c.nw) woff[threadIdx.x] = off;
+    __syncthreads();
     uint32_t wb = 4u * (uint32_t)c.cw / TM_NT;  // old infA words read
     for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
-        const uint32_t nb = (nzb[col >> 5] >> (col & 31)) & 1u;
-        const uint32_t ob = valid ? (ozb[col >> 5] >> (col & 31)) & 1u : 1u;
-        if (nb | ob) {
-            gconf[col] = t.colconf[col];
+        const uint32_t w = nzb[col >> 5];
+        if ((w >> (col & 31)) & 1u) {
+            gval[woff[col >> 5] + __popc(w & ((1u << (col & 31)) - 1u))] = t.colconf[col];
             wb += 4;
         }
     }
@@ -2181,7 +2183,9 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
 #endif
     htm_tm_header* hdr = b.hdr + s;
     uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
-    float* gconf = b.colconf + (size_t)s * c.ncol;
+    float* gconf = b.colconf + (size_t)s * c.ncol;  // dense colConfidence (host-written state)
+    float* gval = b.colval + (size_t)s * c.ncol;    // packed colConfidence (the kernels' write-back)
+    const uint32_t* gnzr = b.colnz + (size_t)s * (c.nw + 1);
     uint16_t* gpat = b.pat + (size_t)s * 2 * HTM_MAXPAT * HTM_MAXACT;
     // ---- load state
     if (!first) {
@@ -2253,8 +2257,9 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
             for (int k = 0; k < ni; k++) pb += 2ull * sh->inf_len[(sh->inf_head + k) % HTM_MAXPAT];
             for (int k = 0; k < nl; k++) pb += 2ull * sh->lrn_len[(sh->lrn_head + k) % HTM_MAXPAT];
             // header in/out, active list, bitmaps in (t-1), colConfidence in (active cols)
+            // (+ the nonzero-column bitmap of colConfidence(t-1))
             sh->bytes = pb + 2ull * sizeof(htm_tm_header) + 2ull * sh->nA + 4ull +
-                        (LEARN ? 3ull : 1ull) * 4ull * c.cw + 4ull * sh->nA;
+                        (LEARN ? 3ull : 1ull) * 4ull * c.cw + 4ull * (c.nw + 1);
         }
     }
     if (first) {
@@ -2269,14 +2274,19 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     }
     __syncthreads();
     const int nA = sh->nA;
-    // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1)),
-    // from HBM on the first step of a run, from LDS after it
+    // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1)):
+    // on the first step of a run its nonzero-column bitmap in HBM (or, after
+    // the host changed the state, the dense copy); from LDS after it
+    const bool from_bm = first && gnzr[c.nw] == 1u;
     const float* pconf = first ? gconf : t.colconf;
+    auto prev_nz = [&](int col) -> bool {
+        return from_bm ? ((gnzr[col >> 5] >> (col & 31)) & 1u) != 0u : pconf[col] != 0.0f;
+    };
     uint32_t hit = 0;
-    for (int a = threadIdx.x; a < nA; a += TM_NT) hit += pconf[sh->act[a]] != 0.0f ? 1u : 0u;
+    for (int a = threadIdx.x; a < nA; a += TM_NT) hit += prev_nz(sh->act[a]) ? 1u : 0u;
     if (keep_prev)
         for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
-            b.prev_pred[(size_t)s * c.ncol + col] = pconf[col] != 0.0f ? 1 : 0;
+            b.prev_pred[(size_t)s * c.ncol + col] = prev_nz(col) ? 1 : 0;
     hit = wg_sum(sh, hit);
     if (threadIdx.x == 0) {
         // computeRawAnomalyScore -> Real32 output
@@ -2325,7 +2335,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     }
     // cell bitmaps: only the words that changed.  infA's previous words are
     // re-read from HBM; on the first step of a run infP1 holds what HBM holds
-    uint32_t wb = write_back_inference(t, first, gbm, gconf, b.colnz + (size_t)s * (c.nw + 1));
+    uint32_t wb = write_back_inference(t, first, gbm, gval, b.colnz + (size_t)s * (c.nw + 1));
     if (LEARN) {
         wg_copy(gbm + 2 * c.cw, t.lrnA, c.cw);
         wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
