@@ -44,6 +44,36 @@ class ScoreGather:
         self.ranges = [shard_range(n_total, self.world, r) for r in range(self.world)]
         self.width = max(b - a for a, b in self.ranges)
         self._pending = []
+        self._pads = {}  # uneven shards: reused padded send buffers (a small ring per shape)
+
+    PAD_RING = 4
+
+    def _padded(self, x):
+        """x [..., n_local] copied into a reused [..., width] zero-padded send
+        buffer.  A ring of PAD_RING buffers per shape: a slot is reused only
+        after the collective that read it last has completed (its handle is
+        waited for), so the async gathers in flight never see a later copy."""
+        import torch
+        key = (tuple(x.shape), x.dtype, str(x.device))
+        ring = self._pads.get(key)
+        if ring is None:
+            shape = tuple(x.shape[:-1]) + (self.width,)
+            ring = self._pads[key] = [[torch.zeros(shape, dtype=x.dtype, device=x.device), None, 0]
+                                      for _ in range(self.PAD_RING)]
+            ring.append(0)  # next slot
+        i = ring[-1]
+        ring[-1] = (i + 1) % self.PAD_RING
+        slot = ring[i]
+        if slot[1] is not None:
+            slot[1].wait()
+            slot[1] = None
+        slot[0][..., :x.shape[-1]].copy_(x)
+        return slot
+
+    @staticmethod
+    def _track(slot, h):
+        if slot is not None:
+            slot[1] = h
 
     @property
     def local_range(self):
@@ -57,10 +87,10 @@ class ScoreGather:
         n = scores.numel()
         if n != self.ranges[self.rank][1] - self.ranges[self.rank][0]:
             raise ValueError("scores do not match this rank's shard")
-        src = scores
+        src, slot = scores, None
         if n != self.width:
-            src = torch.zeros(self.width, dtype=scores.dtype, device=scores.device)
-            src[:n] = scores
+            slot = self._padded(scores)
+            src = slot[0]
         if self.rank == self.dst:
             if staging is None:
                 staging = torch.empty((self.world, self.width), dtype=scores.dtype, device=scores.device)
@@ -68,6 +98,7 @@ class ScoreGather:
         else:
             gl = None
         h = self.dist.gather(src.contiguous(), gather_list=gl, dst=self.dst, group=self.group, async_op=True)
+        self._track(slot, h)
         return h, staging
 
     def gather_rows(self, block, staging=None):
@@ -79,10 +110,10 @@ class ScoreGather:
         m, n = block.shape
         if n != self.ranges[self.rank][1] - self.ranges[self.rank][0]:
             raise ValueError("block does not match this rank's shard")
-        src = block
+        src, slot = block, None
         if n != self.width:
-            src = torch.zeros((m, self.width), dtype=block.dtype, device=block.device)
-            src[:, :n] = block
+            slot = self._padded(block)
+            src = slot[0]
         gl = None
         if self.rank == self.dst:
             if staging is None:
@@ -91,6 +122,7 @@ class ScoreGather:
             if not all(t.is_contiguous() and t.shape == (m, self.width) for t in gl):
                 raise ValueError("staging must hold a contiguous [m, width] block per rank")
         h = self.dist.gather(src.contiguous(), gather_list=gl, dst=self.dst, group=self.group, async_op=True)
+        self._track(slot, h)
         return h, staging
 
     def unpad_rows(self, staging):
