@@ -107,6 +107,18 @@ struct htm_engine {
 };
 
 
+// A/B and tuning knobs read from the environment exist only in the A/B build
+// (make ab -> libhtm_amd_ab.so, -DHTM_AB_KNOBS; tools/ab_libs.py loads it);
+// the product library ignores the environment.
+static const char* ab_knob(const char* name) {
+#ifdef HTM_AB_KNOBS
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 static int flush_deferred(htm_engine* e, hipStream_t st);
 static int flush_sync(htm_engine* e);
 static int densify_conf(htm_engine* e, hipStream_t st);
@@ -291,7 +303,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
     // bitonic key sort at Model-1 sizes
     d.fin_mode = 2;
-    if (const char* env = std::getenv("HTM_TM_FIN"))
+    if (const char* env = ab_knob("HTM_TM_FIN"))
         d.fin_mode = std::strcmp(env, "sorted") == 0 ? 1 : std::strcmp(env, "buckets") == 0 ? 0 : 2;
     // frozen-inference counter window: the union region holds the u8
     // counters (fx_win bytes) plus the active-cell list and its block prefix;
@@ -305,18 +317,18 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // few hundred slots wider can save a whole pass per phase 2 (config 2:
     // 68,376 live segments fit 3 windows of 22,976, not of 22,528)
     size_t gran = 64;
-    if (const char* env = std::getenv("HTM_FX_GRAN")) gran = (size_t)std::max(64, std::atoi(env)) / 64 * 64;  // A/B knob
+    if (const char* env = ab_knob("HTM_FX_GRAN")) gran = (size_t)std::max(64, std::atoi(env)) / 64 * 64;  // A/B knob
     win = (win / gran) * gran;
     if (win < 1024) win = 1024;
     if (win > 64512) win = 64512;
-    if (const char* env = std::getenv("HTM_FX_WIN_MAX"))  // A/B knob: a narrower window (occupancy study)
+    if (const char* env = ab_knob("HTM_FX_WIN_MAX"))  // A/B knob: a narrower window (occupancy study)
         win = std::min(win, (size_t)std::max(1024, std::atoi(env)) / 64 * 64);
     size_t capr = round_up((size_t)d.seg_cap, 64);
     if (win > capr) win = capr;
     d.fx_win = (int32_t)win;
     d.fx_nwin = (int32_t)((d.seg_cap + d.fx_win - 1) / d.fx_win);
     d.fx_pcap = d.fx_win < 65535 ? d.fx_win : 65535;
-    if (const char* env = std::getenv("HTM_FX_PID"))  // A/B knob: 0 = no pid lists (rows path)
+    if (const char* env = ab_knob("HTM_FX_PID"))  // A/B knob: 0 = no pid lists (rows path)
         if (std::atoi(env) == 0) d.fx_pcap = 0;
     d.fx_noff = d.ncells * d.fx_nwin + d.ncells + 1;
     // deferred phase-2 log entries per stream (lockstep): a flush every
@@ -324,7 +336,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // counting in the step); measured on config 2 (profiles/r02_defer):
     // 64 entries flushed every 32 steps 0.273 ms/step, 32 / 16 0.276, 16 / 8 0.304
     d.fx_dcap = n <= 16384 ? 64 : 8;
-    if (const char* env = std::getenv("HTM_DEFER_CAP")) d.fx_dcap = std::max(1, std::atoi(env));  // A/B knob
+    if (const char* env = ab_knob("HTM_DEFER_CAP")) d.fx_dcap = std::max(1, std::atoi(env));  // A/B knob
     return HTM_OK;
 }
 
@@ -470,25 +482,25 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     // three frozen-inference workgroups per CU (HTM_RUN_WAVES): 160 KiB / 3,
     // less the run kernel's static LDS, rounded down to 1 KiB
     size_t budget = optin >= 54 * 1024 ? (size_t)52 * 1024 : (size_t)optin - 2048;
-    if (const char* env = std::getenv("HTM_TM_LDS_BUDGET")) {  // tuning knob (bytes)
+    if (const char* env = ab_knob("HTM_TM_LDS_BUDGET")) {  // tuning knob (bytes)
         long v = std::strtol(env, nullptr, 10);
         if (v >= 16384 && v <= optin) budget = (size_t)v;
     }
-    if (const char* env = std::getenv("HTM_FUSED")) e->fused = std::atoi(env) != 0;  // A/B knob
-    if (const char* env = std::getenv("HTM_RUN_UNIT")) e->run_unit = std::max(1, std::atoi(env));  // A/B knob
-    if (const char* env = std::getenv("HTM_DEFER_DUTY")) e->defer = std::atoi(env) != 0;            // A/B knob
-    if (const char* env = std::getenv("HTM_DEFER_FLUSH_EVERY")) e->flush_every = std::max(1, std::atoi(env));  // test knob
-    if (const char* env = std::getenv("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
-    if (const char* env = std::getenv("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
-    if (const char* env = std::getenv("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
+    if (const char* env = ab_knob("HTM_FUSED")) e->fused = std::atoi(env) != 0;  // A/B knob
+    if (const char* env = ab_knob("HTM_RUN_UNIT")) e->run_unit = std::max(1, std::atoi(env));  // A/B knob
+    if (const char* env = ab_knob("HTM_DEFER_DUTY")) e->defer = std::atoi(env) != 0;            // A/B knob
+    if (const char* env = ab_knob("HTM_DEFER_FLUSH_EVERY")) e->flush_every = std::max(1, std::atoi(env));  // test knob
+    if (const char* env = ab_knob("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
+    if (const char* env = ab_knob("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
+    if (const char* env = ab_knob("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
-    if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
+    if (r && !ab_knob("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
         // shapes whose fixed LDS state leaves no room at 3 workgroups per CU
         // (e.g. 32 cells per column) run at 2
         budget = (size_t)76 * 1024;
         r = derive(*cfg, n_streams, budget, e->dc);
     }
-    if (r && !std::getenv("HTM_TM_LDS_BUDGET") && optin > 78 * 1024) {
+    if (r && !ab_knob("HTM_TM_LDS_BUDGET") && optin > 78 * 1024) {
         // 4096 columns (config 5): one workgroup per CU
         budget = (size_t)optin - 2048;
         r = derive(*cfg, n_streams, budget, e->dc);

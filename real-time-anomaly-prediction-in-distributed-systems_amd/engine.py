@@ -11,7 +11,6 @@ ModelTesting.py; this engine replaces that per-stream loop.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -51,8 +50,8 @@ class HTMEngine:
         self.sdr_words = (cfg.sdr_bits + 31) // 32
         self.sp_learn = True
         self.tm_learn = True
-        # the engine's default (HTM_OPT_FUSED); SDR-input engines always run unfused
-        self.fused = os.environ.get("HTM_FUSED", "1") != "0" and not self.sdr_bits
+        # the engine's default (HTM_OPT_FUSED on); SDR-input engines always run unfused
+        self.fused = not self.sdr_bits
         self.is_fleet = bool(self._L.htm_is_fleet(self.h))
         if self.is_fleet:
             self.sp_learn = self.tm_learn = False

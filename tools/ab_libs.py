@@ -1,7 +1,9 @@
 """A/B of library builds on one box: lockstep ms/step of the config-2
 workload, each build in its own process (HTM_AMD_LIB_VARIANT), interleaved
 over rounds (cdna_hip_programming.md §5.4 rule 24: same box, alternating).
-usage: python tools/ab_libs.py <variant|main>[@ENV=VAL...] ...   (main = libhtm_amd.so)"""
+usage: python tools/ab_libs.py <variant|main>[@ENV=VAL...] ...   (main = libhtm_amd.so)
+The engine reads ENV=VAL knobs only in builds with -DHTM_AB_KNOBS: "ab@HTM_FLUSH_WG=64"
+(make -C <pkg>/csrc ab -> libhtm_amd_ab.so); "main@..." is refused."""
 import json
 import os
 import subprocess
@@ -45,6 +47,8 @@ for r in range(rounds):
         env = dict(os.environ)
         env.pop("HTM_AMD_LIB_VARIANT", None)
         lib, *kv = v.split("@")  # "<build>@ENV=VAL@..." sets engine env knobs too
+        if kv and lib == "main":
+            sys.exit("env knobs need the A/B build: use ab@... (make ab)")
         if lib != "main":
             env["HTM_AMD_LIB_VARIANT"] = lib
         for x in kv:
