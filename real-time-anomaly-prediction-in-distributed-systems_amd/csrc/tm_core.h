@@ -102,7 +102,7 @@ struct Tm {
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR
+    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -1213,9 +1213,14 @@ __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
         collect_frozen(t, t.c.act_thr, FX_PID);
         __syncthreads();
         const uint32_t npc = count_predicted_cols(t);
+        STAMP(t, SB_CPC);
         const bool inSeq = (double)npc >= 0.5 * sh->avg_dens;
         const bool keep = need == P2_IF_IN_SEQ && inSeq;
-        if (!keep && defer_phase2(t)) return inSeq;
+        if (!keep) {
+            const bool logged = defer_phase2(t);
+            STAMP(t, SB_DEFER);
+            if (logged) return inSeq;
+        }
         collect_frozen(t, t.c.act_thr, FX_WIN_REUSE);
         __syncthreads();
         if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)t.c.q_cap) {

@@ -276,7 +276,7 @@ class HTMEngine:
         out = (ctypes.c_uint64 * 48)()
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
-                 "scan", "sort", "sums", "owner", "sload", "count", "fclr"]
+                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer"]
         cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
         return dict(cycles={k: int(out[i]) for i, k in enumerate(names)},
                     counts={k: int(out[24 + i]) for i, k in enumerate(cnames)},
