@@ -57,10 +57,11 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t p1_n;       // their number, or -1 when infA is not phase 1's
     float tf[4];
     uint32_t red[3 * TM_NWAVES];
+    uint32_t nz_valid;  // the loaded nonzero-column bitmap of colConfidence(t-1) is current (first step)
     uint16_t act[HTM_MAXACT];
     uint32_t cand[HTM_MAXACT];
     uint32_t newsrc[HTM_MAXSYN];
-    uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
+    __attribute__((aligned(16))) uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
 #ifdef HTM_STAMPS
     uint64_t st_acc[HTM_NSTAMP], st_cnt[HTM_NSTAMP], st_last, st_start;
 #endif
@@ -2083,35 +2084,20 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     t.defer = FROZEN && b.fx_dlog != nullptr;
 }
 
-// Write the inference state back to HBM, touching only what changed:
-// infActiveState words that differ from HBM (the old words are loaded first,
-// their latency hidden behind the colConfidence bitmap), infPredictedState
-// words that differ from infP(t-1) (on the first step of a run the LDS copy
-// is what HBM holds), and colConfidence PACKED: gnz[0..nw) is the bitmap of
-// its nonzero columns and gval[0..n) their values in ascending column order
-// (one contiguous run of stores, not a scatter over the dense columns);
-// gnz[nw] == 1 says the packed form is current (the host densifies it into
-// TmBufs::colconf before it reads or replaces the state, then clears the
-// flag, and the next step starts from the dense copy).  Uses t.flags and the
-// head of t.U (free after the TM step).  Returns the bytes this thread moved.
-// Contains barriers.
-__device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint32_t* gbm, float* gval,
-                                                         uint32_t* gnz) {
+// Write the inference state back to HBM without reading anything: the
+// infActiveState and infPredictedState bitmaps whole (coalesced 16-byte
+// stores; a step changes the words of ~80 columns of each, which as scattered
+// 4-byte stores cost a 32-byte sector apiece -- the same bytes, plus a read of
+// the old words to find them), and colConfidence PACKED: gnz[0..nw) is the
+// bitmap of its nonzero columns and gval[0..n) their values in ascending
+// column order (one contiguous run of stores, not a scatter over the dense
+// columns); gnz[nw] == 1 says the packed form is current (the host densifies
+// it into TmBufs::colconf before it reads or replaces the state, then clears
+// the flag, and the next step starts from the dense copy).  Uses t.flags and
+// the head of t.U (free after the TM step).  Returns the bytes this thread
+// moved.  Contains barriers.
+__device__ __forceinline__ uint32_t write_back_inference(Tm& t, uint32_t* gbm, float* gval, uint32_t* gnz) {
     const DevCfg& c = t.c;
-    constexpr int PER = 4;  // old infA words prefetched per thread (all of them up to 32,768 cells)
-    uint32_t olda[PER];
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        olda[j] = w < c.cw ? gbm[w] : 0u;
-    }
-    uint32_t oldnz[(HTM_MAXNW + TM_NT - 1) / TM_NT];
-#pragma unroll
-    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        oldnz[j] = w < c.nw ? gnz[w] : 0u;
-    }
-    const bool valid = gnz[c.nw] == 1u;
     uint32_t* nzb = t.flags;  // the new bitmap
     uint32_t* woff = t.U;     // packed position of each bitmap word's first column
     // nonzero-column bitmap of the LDS colConfidence (ballots over 64 columns)
@@ -2123,45 +2109,34 @@ __device__ __forceinline__ uint32_t write_back_inference(Tm& t, bool first, uint
             if (col0 + 32 < c.ncol) nzb[(col0 >> 5) + 1] = (uint32_t)(bal >> 32);
         }
     }
+    // the cell bitmaps meanwhile (they are final): consecutive words per lane,
+    // 256 contiguous bytes per wave store (16-byte lanes through these LDS
+    // pointers trip an LLVM gfx950 verifier error in the paged kernel)
+    uint32_t wb = 0;
+    for (int w = threadIdx.x; w < c.cw; w += TM_NT) {
+        gbm[w] = t.infA[w];
+        gbm[c.cw + w] = t.infP[w];
+        wb += 8;
+    }
     __syncthreads();
     // word offsets: exclusive prefix of the words' popcounts (nw <= 128 < TM_NT)
     uint32_t tot;
     const uint32_t mine = threadIdx.x < (uint32_t)c.nw ? (uint32_t)__popc(nzb[threadIdx.x]) : 0u;
     const uint32_t off = wg_excl_scan(t.sh, mine, &tot);
-    if (threadIdx.x < (uint32_t)c.nw) woff[threadIdx.x] = off;
+    if (threadIdx.x < (uint32_t)c.nw) {
+        woff[threadIdx.x] = off;
+        gnz[threadIdx.x] = nzb[threadIdx.x];
+        wb += 4;
+    }
+    if (threadIdx.x == 0) {
+        gnz[c.nw] = 1u;
+        wb += 4;
+    }
     __syncthreads();
-    uint32_t wb = 4u * (uint32_t)c.cw / TM_NT;  // old infA words read
     for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
         const uint32_t w = nzb[col >> 5];
         if ((w >> (col & 31)) & 1u) {
             gval[woff[col >> 5] + __popc(w & ((1u << (col & 31)) - 1u))] = t.colconf[col];
-            wb += 4;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < (HTM_MAXNW + TM_NT - 1) / TM_NT; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        if (w < c.nw && (!valid || oldnz[j] != nzb[w])) {
-            gnz[w] = nzb[w];
-            wb += 4;
-        }
-    }
-    if (threadIdx.x == 0 && !valid) gnz[c.nw] = 1u;
-    for (int j = 0; threadIdx.x + j * TM_NT < (uint32_t)c.cw; j++) {
-        const int w = threadIdx.x + j * TM_NT;
-        uint32_t o = 0;
-#pragma unroll
-        for (int i = 0; i < PER; i++)
-            if (i == j) o = olda[i];
-        if (j >= PER) o = gbm[w];
-        const uint32_t v = t.infA[w];
-        if (o != v) {
-            gbm[w] = v;
-            wb += 4;
-        }
-        const uint32_t p = t.infP[w];
-        if (!first || t.infP1[w] != p) {
-            gbm[c.cw + w] = p;
             wb += 4;
         }
     }
@@ -2209,83 +2184,81 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         __syncthreads();
         if (threadIdx.x == 0) sh->bytes += 2ull * sh->nA;
     }
-    if (first && threadIdx.x == 0) {
-        sh->bytes_acc = 0;
-        sh->avg_dens = hdr->avg_input_density;
-        sh->avg_lsl = hdr->avg_learned_seq_length;
-        sh->lrn_iter = hdr->lrn_iter;
-        sh->iter = hdr->iter;
-        sh->pam = hdr->pam_counter;
-        sh->lsl = hdr->learned_seq_length;
-        sh->reset = hdr->reset_called;
-        sh->have_avg = hdr->have_avg_density;
-        sh->rf = hdr->rng_f;
-        sh->rr = hdr->rng_r;
-        sh->hwm = hdr->seg_hwm;
-        sh->nlive = hdr->seg_live;
-        sh->n_inf_pat = hdr->n_inf_pat;
-        sh->n_lrn_pat = hdr->n_lrn_pat;
-        sh->inf_head = hdr->inf_pat_head;
-        sh->lrn_head = hdr->lrn_pat_head;
-        sh->n_upd = hdr->n_upd;
-        sh->err = hdr->error;
-        sh->st[0] = hdr->stat_inf_phase2;
-        sh->st[1] = hdr->stat_inf_backtrack;
-        sh->st[2] = hdr->stat_lrn_phase2;
-        sh->st[3] = hdr->stat_lrn_backtrack;
-        uint32_t na = sp.nact[s];
-        sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
-    }
-    if (first && threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
-    if (first && threadIdx.x < HTM_MAXPAT) {
-        sh->inf_len[threadIdx.x] = hdr->inf_pat_len[threadIdx.x];
-        sh->lrn_len[threadIdx.x] = hdr->lrn_pat_len[threadIdx.x];
-    }
-    if (first && threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
-    __syncthreads();
-    // live pattern-history entries only (ring slots head .. head+n-1)
     if (first) {
-        const int ni = sh->n_inf_pat, nl = LEARN ? sh->n_lrn_pat : 0;
-        for (int i = threadIdx.x; i < (ni + nl) * HTM_MAXACT; i += TM_NT) {
-            const int k = i / HTM_MAXACT, a = i % HTM_MAXACT;
-            if (k < ni) {
-                const int slot = (sh->inf_head + k) % HTM_MAXPAT;
-                if (a < sh->inf_len[slot]) sh->inf_pat[slot][a] = gpat[slot * HTM_MAXACT + a];
-            } else {
-                const int slot = (sh->lrn_head + k - ni) % HTM_MAXPAT;
-                if (a < sh->lrn_len[slot])
-                    t.lrnpat[slot][a] = gpat[(HTM_MAXPAT + slot) * HTM_MAXACT + a];
+        // every load of the state is issued before any is used (one round
+        // trip): header scalars, RNG, the whole pattern ring(s) (2 KiB each,
+        // 16-byte loads; dead slots come along), infP(t-1), and the
+        // nonzero-column bitmap of colConfidence(t-1) with its valid flag
+        if (threadIdx.x == 0) {
+            sh->bytes_acc = 0;
+            sh->avg_dens = hdr->avg_input_density;
+            sh->avg_lsl = hdr->avg_learned_seq_length;
+            sh->lrn_iter = hdr->lrn_iter;
+            sh->iter = hdr->iter;
+            sh->pam = hdr->pam_counter;
+            sh->lsl = hdr->learned_seq_length;
+            sh->reset = hdr->reset_called;
+            sh->have_avg = hdr->have_avg_density;
+            sh->rf = hdr->rng_f;
+            sh->rr = hdr->rng_r;
+            sh->hwm = hdr->seg_hwm;
+            sh->nlive = hdr->seg_live;
+            sh->n_inf_pat = hdr->n_inf_pat;
+            sh->n_lrn_pat = hdr->n_lrn_pat;
+            sh->inf_head = hdr->inf_pat_head;
+            sh->lrn_head = hdr->lrn_pat_head;
+            sh->n_upd = hdr->n_upd;
+            sh->err = hdr->error;
+            sh->st[0] = hdr->stat_inf_phase2;
+            sh->st[1] = hdr->stat_inf_backtrack;
+            sh->st[2] = hdr->stat_lrn_phase2;
+            sh->st[3] = hdr->stat_lrn_backtrack;
+            uint32_t na = sp.nact[s];
+            sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
+            sh->nz_valid = gnzr[c.nw];
+        }
+        if (threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
+        if (threadIdx.x < HTM_MAXPAT) {
+            sh->inf_len[threadIdx.x] = hdr->inf_pat_len[threadIdx.x];
+            sh->lrn_len[threadIdx.x] = hdr->lrn_pat_len[threadIdx.x];
+        }
+        if (threadIdx.x < HTM_MAXACT) sh->act[threadIdx.x] = sp.act[(size_t)s * HTM_MAXACT + threadIdx.x];
+        constexpr int RINGW = HTM_MAXPAT * HTM_MAXACT / 2;  // 32-bit words per ring
+        const uint32_t* gpw = reinterpret_cast<const uint32_t*>(gpat);
+        for (int i = threadIdx.x; i < RINGW; i += TM_NT) {
+            reinterpret_cast<uint32_t*>(&sh->inf_pat[0][0])[i] = gpw[i];
+            if (LEARN) reinterpret_cast<uint32_t*>(&t.lrnpat[0][0])[i] = gpw[RINGW + i];
+        }
+        for (int w = threadIdx.x; w < c.cw; w += TM_NT) {
+            const uint32_t p = gbm[c.cw + w];  // infPredictedState t -> t-1
+            t.infP1[w] = p;
+            t.infP[w] = p;
+            if (LEARN) {
+                const uint32_t la = gbm[2 * c.cw + w], lp = gbm[3 * c.cw + w];
+                t.lrnA1[w] = la;  // lrnActiveState t -> t-1
+                t.lrnA[w] = la;
+                t.lrnP1[w] = lp;  // lrnPredictedState t -> t-1
+                t.lrnP[w] = lp;
             }
         }
+        if (threadIdx.x < (uint32_t)c.nw) t.flags[threadIdx.x] = gnzr[threadIdx.x];
+        __syncthreads();
         if (threadIdx.x == 0) {
-            unsigned long long pb = 0;
-            for (int k = 0; k < ni; k++) pb += 2ull * sh->inf_len[(sh->inf_head + k) % HTM_MAXPAT];
-            for (int k = 0; k < nl; k++) pb += 2ull * sh->lrn_len[(sh->lrn_head + k) % HTM_MAXPAT];
-            // header in/out, active list, bitmaps in (t-1), colConfidence in (active cols)
-            // (+ the nonzero-column bitmap of colConfidence(t-1))
-            sh->bytes = pb + 2ull * sizeof(htm_tm_header) + 2ull * sh->nA + 4ull +
+            // header in/out, active list, pattern ring(s), bitmaps in (t-1), the
+            // nonzero-column bitmap of colConfidence(t-1) + flag
+            sh->bytes = (LEARN ? 2ull : 1ull) * 4ull * RINGW + 2ull * sizeof(htm_tm_header) + 2ull * sh->nA + 4ull +
                         (LEARN ? 3ull : 1ull) * 4ull * c.cw + 4ull * (c.nw + 1);
         }
     }
-    if (first) {
-        wg_copy(t.infP1, gbm + c.cw, c.cw);  // infPredictedState t -> t-1
-        wg_copy(t.infP, gbm + c.cw, c.cw);
-        if (LEARN) {
-            wg_copy(t.lrnA1, gbm + 2 * c.cw, c.cw);  // lrnActiveState t -> t-1
-            wg_copy(t.lrnP1, gbm + 3 * c.cw, c.cw);  // lrnPredictedState t -> t-1
-            wg_copy(t.lrnA, gbm + 2 * c.cw, c.cw);
-            wg_copy(t.lrnP, gbm + 3 * c.cw, c.cw);
-        }
-    }
-    __syncthreads();
     const int nA = sh->nA;
     // ---- anomaly input: prevPredictedColumns = nonzero(colConfidence(t-1)):
-    // on the first step of a run its nonzero-column bitmap in HBM (or, after
-    // the host changed the state, the dense copy); from LDS after it
-    const bool from_bm = first && gnzr[c.nw] == 1u;
+    // on the first step of a run its nonzero-column bitmap (loaded into
+    // t.flags; after the host changed the state, the dense copy in HBM); from
+    // LDS after it
+    const bool from_bm = first && sh->nz_valid == 1u;
     const float* pconf = first ? gconf : t.colconf;
     auto prev_nz = [&](int col) -> bool {
-        return from_bm ? ((gnzr[col >> 5] >> (col & 31)) & 1u) != 0u : pconf[col] != 0.0f;
+        return from_bm ? ((t.flags[col >> 5] >> (col & 31)) & 1u) != 0u : pconf[col] != 0.0f;
     };
     uint32_t hit = 0;
     for (int a = threadIdx.x; a < nA; a += TM_NT) hit += prev_nz(sh->act[a]) ? 1u : 0u;
@@ -2340,7 +2313,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     }
     // cell bitmaps: only the words that changed.  infA's previous words are
     // re-read from HBM; on the first step of a run infP1 holds what HBM holds
-    uint32_t wb = write_back_inference(t, first, gbm, gval, b.colnz + (size_t)s * (c.nw + 1));
+    uint32_t wb = write_back_inference(t, gbm, gval, b.colnz + (size_t)s * (c.nw + 1));
     if (LEARN) {
         wg_copy(gbm + 2 * c.cw, t.lrnA, c.cw);
         wg_copy(gbm + 3 * c.cw, t.lrnP, c.cw);
