@@ -195,9 +195,10 @@ int htm_counters(htm_engine* eng, uint64_t* out8);
 
 /* Diagnostic builds only (libhtm_amd_stamps.so, -DHTM_STAMPS): per-phase
  * shader-cycle stamps of the TM kernel summed over streams since the last
- * call (out48[0..23]) and event counts (out48[24..47]); HTM_E_STATE in the
- * product library. */
-int htm_debug_stamps(htm_engine* eng, uint64_t* out48);
+ * call (out96[0..23]) and event counts (out96[24..47]), then the same over
+ * the tail steps only -- stream-steps whose TM part took >= 2^18 cycles
+ * (out96[48..95]); HTM_E_STATE in the product library. */
+int htm_debug_stamps(htm_engine* eng, uint64_t* out96);
 
 /* Synchronise and check every stream's overflow flags (HTM_E_CAPACITY). */
 int htm_status(htm_engine* eng);

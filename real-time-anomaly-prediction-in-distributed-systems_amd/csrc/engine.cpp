@@ -336,7 +336,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // counting in the step); measured on config 2 (profiles/r02_defer):
     // 64 entries flushed every 32 steps 0.273 ms/step, 32 / 16 0.276, 16 / 8 0.304
     d.fx_dcap = n <= 16384 ? 64 : 8;
-    if (const char* env = ab_knob("HTM_DEFER_CAP")) d.fx_dcap = std::max(1, std::atoi(env));  // A/B knob
+    if (const char* env = ab_knob("HTM_DEFER_CAP")) d.fx_dcap = std::min(64, std::max(1, std::atoi(env)));  // A/B knob (the flush's job builder handles <= 64)
     return HTM_OK;
 }
 
@@ -416,7 +416,7 @@ static int allocate(htm_engine* e) {
     ALLOC(e->tm.fx_base, uint64_t, S);
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
-    ALLOC(e->tm.dbg, uint64_t, S * 2 * HTM_NSTAMP);
+    ALLOC(e->tm.dbg, uint64_t, S * 4 * HTM_NSTAMP);
 #endif
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
@@ -670,7 +670,7 @@ static int alloc_dlog(htm_engine* e) {
     }
     HIP_TRY(hipEventCreateWithFlags(&e->ev_logged, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_flushed, hipEventDisableTiming));
-    ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * (size_t)d.max_act_cells);  // last: the "allocated" test
+    ALLOC(e->tm.fx_dlog, uint16_t, S * (size_t)d.fx_dcap * fx_dstride(d));  // last: the "allocated" test
     return HTM_OK;
 }
 
@@ -981,16 +981,16 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
     return HTM_OK;
 }
 
-int htm_debug_stamps(htm_engine* e, uint64_t* out48) {
-    if (!e || !out48) return htm_fail(HTM_E_INVALID, "bad arguments");
+int htm_debug_stamps(htm_engine* e, uint64_t* out96) {
+    if (!e || !out96) return htm_fail(HTM_E_INVALID, "bad arguments");
     if (!e->tm.dbg) return htm_fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
     HIP_TRY(hipDeviceSynchronize());
-    const int W = 2 * HTM_NSTAMP;
+    const int W = 4 * HTM_NSTAMP;
     std::vector<uint64_t> h((size_t)e->n * W);
     HIP_TRY(hipMemcpy(h.data(), e->tm.dbg, h.size() * 8, hipMemcpyDeviceToHost));
-    for (int k = 0; k < W; k++) out48[k] = 0;
+    for (int k = 0; k < W; k++) out96[k] = 0;
     for (int s = 0; s < e->n; s++)
-        for (int k = 0; k < W; k++) out48[k] += h[(size_t)s * W + k];
+        for (int k = 0; k < W; k++) out96[k] += h[(size_t)s * W + k];
     HIP_TRY(hipMemset(e->tm.dbg, 0, h.size() * 8));
     return HTM_OK;
 }

@@ -87,6 +87,11 @@ struct DevCfg {
     double rdse_res;                      // RDSE resolution
 };
 
+// deferred-log slot stride in cells: max_act_cells rounded up to 8, so every
+// slot starts 16-byte aligned (the flush's job builder compares slots in
+// 16-byte loads)
+__host__ __device__ inline size_t fx_dstride(const DevCfg& c) { return ((size_t)c.max_act_cells + 7) & ~(size_t)7; }
+
 #define ENC_LIST 128        // u16 words per (step, stream) encoded input list: count, then the bits
 #define RDSE_HDR_WORDS 64   // int32 words of an RDSE field header (HTM_ST_ENC_RDSE)
 

@@ -376,7 +376,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         __syncthreads();
         const size_t ei = (size_t)s * c.fx_dcap + i;
         const uint32_t len = b.fx_dlen[ei];
-        const uint16_t* cl = b.fx_dlog + ei * (size_t)c.max_act_cells;
+        const uint16_t* cl = b.fx_dlog + ei * fx_dstride(c);
         for (uint32_t k = threadIdx.x; k < len; k += TM_NT) atomicOr(&t.infA[cl[k] >> 5], 1u << (cl[k] & 31));
         __syncthreads();
         collect_frozen(t, c.act_thr, FX_WIN);
@@ -390,17 +390,71 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
     }
 }
 
-// before a flush (on the flush's stream): the entries [fx_dflushed, fx_dsnap)
-// of every stream as a compact job list, so the flush's workgroups claim
-// only real entries
-__global__ void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const uint32_t f = b.fx_dflushed[s], p = b.fx_dsnap[s] - f;
-    if (!p) return;
-    const uint32_t base = atomicAdd(&b.fx_fwork[2], p);
+// Before a flush (on the flush's stream): the entries [fx_dflushed, fx_dsnap)
+// of every stream as a compact job list, without repeats -- an entry whose
+// active set equals an earlier entry of the same batch (order-independent
+// hash and length first, then the cells themselves) is dropped: the flush of
+// the earlier one makes the same one-time record writes.  Steps append to the
+// ring beside this kernel but never into [fx_dflushed, fx_dsnap), so the
+// batch is stable.  One workgroup per stream.
+__global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n) {
+    __shared__ uint32_t hsh[64], len[64], keep[64];
+    const int s = blockIdx.x;
+    const uint32_t f = b.fx_dflushed[s], p = b.fx_dsnap[s] - f;  // p <= fx_dcap <= 64
+    if (p == 0 || p > 64) return;
     const uint32_t dcap = (uint32_t)c.fx_dcap;
-    for (uint32_t d = 0; d < p; d++) b.fx_fjobs[base + d] = (uint32_t)s * dcap + (f + d) % dcap;
+    const size_t mac = fx_dstride(c);
+    auto entry = [&](uint32_t i) { return (size_t)s * dcap + (f + i) % dcap; };
+    if (threadIdx.x < p) {
+        hsh[threadIdx.x] = 0u;
+        len[threadIdx.x] = b.fx_dlen[entry(threadIdx.x)];
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i < p; i++) {
+        const uint16_t* cl = b.fx_dlog + entry(i) * mac;
+        uint32_t h = 0;
+        for (uint32_t k = threadIdx.x; k < len[i]; k += blockDim.x) h += fmix32(cl[k] + 0x9e3779b9u);
+        h = wave_sum_u32(h);
+        if (lane_id() == 0 && h) atomicAdd(&hsh[i], h);
+    }
+    __syncthreads();
+    if (threadIdx.x < p) {
+        const uint32_t i = threadIdx.x, li = len[i];
+        const uint16_t* ci = b.fx_dlog + entry(i) * mac;
+        uint32_t dup = 0;
+        for (uint32_t j = 0; j < i && !dup; j++) {
+            if (hsh[j] != hsh[i] || len[j] != li) continue;
+            const uint16_t* cj = b.fx_dlog + entry(j) * mac;
+            // 8 cells per 16-byte load, four loads in flight (slots are 16-byte
+            // aligned: max_act_cells is a multiple of 8)
+            const uint4* qi = reinterpret_cast<const uint4*>(ci);
+            const uint4* qj = reinterpret_cast<const uint4*>(cj);
+            const uint32_t nq = li / 8;
+            uint32_t diff = 0;
+            for (uint32_t q = 0; q < nq && !diff; q += 4) {
+                uint4 a[4], z[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    a[u] = q + u < nq ? qi[q + u] : make_uint4(0u, 0u, 0u, 0u);
+                    z[u] = q + u < nq ? qj[q + u] : make_uint4(0u, 0u, 0u, 0u);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    diff |= (a[u].x ^ z[u].x) | (a[u].y ^ z[u].y) | (a[u].z ^ z[u].z) | (a[u].w ^ z[u].w);
+            }
+            for (uint32_t k = nq * 8; k < li && !diff; k++) diff = ci[k] != cj[k];
+            dup = diff ? 0u : 1u;
+        }
+        keep[i] = dup ? 0u : 1u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < p; i++) m += keep[i];
+        uint32_t base = atomicAdd(&b.fx_fwork[2], m);
+        for (uint32_t i = 0; i < p; i++)
+            if (keep[i]) b.fx_fjobs[base++] = (uint32_t)s * dcap + (f + i) % dcap;
+    }
 }
 
 // after a flush: every snapshot entry is flushed; the counters restart
@@ -432,7 +486,7 @@ int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipS
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
-    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c, b, n);
+    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3(n), dim3(256), 0, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -52,18 +52,18 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t ti[8];
     int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
     int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
-    uint32_t fx_n, fx_f; // deferred log: entries logged, entries flushed (thread 0's copies)
     uint32_t p1_off;    // LDS offset of the active columns (ascending) phase 1 built infA from
     int32_t p1_n;       // their number, or -1 when infA is not phase 1's
     float tf[4];
     uint32_t red[3 * TM_NWAVES];
     uint32_t nz_valid;  // the loaded nonzero-column bitmap of colConfidence(t-1) is current (first step)
+    uint32_t acc[3];    // wg_sum1's rotating accumulators
     uint16_t act[HTM_MAXACT];
     uint32_t cand[HTM_MAXACT];
     uint32_t newsrc[HTM_MAXSYN];
     __attribute__((aligned(16))) uint16_t inf_pat[HTM_MAXPAT][HTM_MAXACT];
 #ifdef HTM_STAMPS
-    uint64_t st_acc[HTM_NSTAMP], st_cnt[HTM_NSTAMP], st_last, st_start;
+    uint64_t st_acc[HTM_NSTAMP], st_cnt[HTM_NSTAMP], st_last, st_start, st_sp0;
 #endif
 };
 
@@ -98,12 +98,15 @@ struct Tm {
     uint32_t nr;       // ranks (live segments) of the frozen index
     const TmBufs* tb;  // the engine's buffers (deferred-duty log)
     bool defer;        // discarded frozen phase 2s log their active cells (TmBufs::fx_dlog)
+    uint32_t dn, df;   // deferred log: entries logged, entries flushed (every thread's copy)
+    uint32_t rh, rl;   // hash and length of the set in ring slot (threadIdx.x % 64) (slots < fx_dcap)
+    uint32_t nsum;     // wg_sum1 calls so far (every thread's copy)
 };
 
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER
+    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER, SB_SP
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -187,6 +190,13 @@ __device__ __forceinline__ uint32_t wg_sum(TmSh* sh, uint32_t v) {
     __syncthreads();
     return t;
 }
+// Sum over the workgroup with ONE barrier: the waves add into one of three
+// rotating LDS accumulators; after the barrier every thread reads it and
+// thread 0 zeroes the slot the call after next uses (its last readers read it
+// before this call's barrier).  tm_bind zeroes the slots; every thread counts
+// the calls (t.nsum).  Call uniformly.
+__device__ __forceinline__ uint32_t wg_sum1(Tm& t, uint32_t v);
+
 // The same with one barrier, through its own slots of sh->red: callers must
 // have passed another barrier since the previous call read them.
 __device__ __forceinline__ uint32_t wg_excl_scan1(TmSh* sh, uint32_t v, uint32_t* total);
@@ -221,6 +231,18 @@ __device__ __forceinline__ uint32_t wg_excl_scan1(TmSh* sh, uint32_t v, uint32_t
     }
     *total = tot;
     return base + incl - v;
+}
+
+__device__ __forceinline__ uint32_t wg_sum1(Tm& t, uint32_t v) {
+    uint32_t* acc = t.sh->acc;
+    const uint32_t k = t.nsum % 3u;
+    v = wave_sum_u32(v);
+    if (lane_id() == 0 && v) atomicAdd(&acc[k], v);
+    __syncthreads();
+    const uint32_t r = acc[k];
+    if (threadIdx.x == 0) acc[(k + 2u) % 3u] = 0u;
+    t.nsum++;
+    return r;
 }
 
 __device__ __forceinline__ uint32_t col_of(const DevCfg& c, uint32_t cell) { return __umulhi(cell, c.kmagic); }
@@ -280,7 +302,10 @@ __device__ __forceinline__ uint32_t wg_bitmap_list(Tm& t, const uint32_t* bm, ui
 // ---------------------------------------------------------------------------
 // Inference
 // _inferPhase1(activeColumns, useStartCells)
-__device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start) {
+// prevP: the predicted state it reads (default infPredictedState(t-1); a
+// backtrack replay passes the previous replay's infP directly)
+__device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA, bool use_start,
+                                             const uint32_t* prevP = nullptr) {
     const int K = t.c.K;
     if (threadIdx.x == 0) {  // (collect_frozen lists the active cells column by column)
         t.sh->p1_off = (uint32_t)(reinterpret_cast<const char*>(cols) - reinterpret_cast<const char*>(t.sh));
@@ -294,7 +319,7 @@ __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA
         if (use_start) {
             bm_or_field(t.infA, lo, 1, 1u);
         } else {
-            uint32_t f = bm_field(t.infP1, lo, K);
+            uint32_t f = bm_field(prevP ? prevP : t.infP1, lo, K);
             if (f) {
                 bm_or_field(t.infA, lo, K, f);
                 npc++;
@@ -303,7 +328,7 @@ __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA
             }
         }
     }
-    npc = wg_sum(t.sh, npc);
+    npc = wg_sum1(t, npc);
     STAMP(t, SB_P1);
     return use_start || (double)npc >= 0.50 * (double)nA;
 }
@@ -754,7 +779,7 @@ __device__ __forceinline__ uint32_t count_predicted_cols(Tm& t) {
     uint32_t n = 0;
     for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
         if (bm_field(t.infP, (uint32_t)col * c.K, c.K)) n++;
-    return wg_sum(t.sh, n);
+    return wg_sum1(t, n);
 }
 
 // Tail of _inferPhase2 for qn <= q_lds (<= 1024) qualifying segments: the
@@ -859,7 +884,7 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
             gdc[k] = dc;
         }
     });
-    nb = wg_sum(sh, nb);  // (barriers)
+    nb = wg_sum1(t, nb);  // (a barrier)
     if (threadIdx.x == 0) sh->bytes += nb;
     STAMP(t, SB_FIN1);
     COUNT(t, SC_QN, qn);
@@ -1136,62 +1161,59 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 // makes its qualifying segments' dutyCycle() record writes.  The log is a
 // ring of fx_dcap entries per stream; an active set equal to one still in the
 // ring (flushed or not: backtrack replays recur from step to step) is not
-// logged again -- its writes are made or pending.  False when the ring holds
-// fx_dcap unflushed entries: the caller then counts the rank windows itself.
-// Contains barriers: call uniformly.
+// logged again -- its writes are made or pending.  The ring's hashes and
+// lengths live in registers (lane l of every wave holds slot l's, loaded with
+// the state), so finding the candidate costs no memory access; only the
+// newest candidate's cells are read back and compared in full.  False when
+// the ring holds fx_dcap unflushed entries: the caller then counts the rank
+// windows itself.  Contains barriers: call uniformly.
 __device__ __forceinline__ bool defer_phase2(Tm& t) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const TmBufs& b = *t.tb;
     const uint32_t dcap = (uint32_t)c.fx_dcap;
     const uint32_t na = (uint32_t)sh->fx_na;
-    const uint32_t mac = (uint32_t)c.max_act_cells;
     const uint16_t* cells = reinterpret_cast<const uint16_t*>(t.U + c.fx_win / 4 + 64);
-    const size_t s = (size_t)t.s;
+    const size_t stride = fx_dstride(c);
     // order-independent hash of the set
     uint32_t h = 0;
     for (uint32_t k = threadIdx.x; k < na; k += TM_NT) h += fmix32(cells[k] + 0x9e3779b9u);
-    if (threadIdx.x == 0) {  // (the counters are written by thread 0 only)
-        sh->fx_n = b.fx_dn[s];
-        sh->fx_f = b.fx_dflushed[s];
-    }
-    h = fmix32(wg_sum(sh, h) ^ na);
-    const uint32_t n = sh->fx_n, f = sh->fx_f;
-    // the resident entries whose hash and length match: the newest one is compared in full
+    h = fmix32(wg_sum1(t, h) ^ na);
+    const uint32_t n = t.dn;
+    // the newest resident entry with this hash and length (every wave finds
+    // the same: lane l of each wave holds slot l)
+    const uint32_t l = lane_id();
     const uint32_t resident = n < dcap ? n : dcap;
-    uint32_t cand = 0xFFFFFFFFu;
-    for (uint32_t i = threadIdx.x; i < resident; i += TM_NT) {
-        const uint32_t e = n - 1u - i;
-        const size_t slot = s * dcap + e % dcap;
-        if (b.fx_dhash[slot] == h && b.fx_dlen[slot] == na) cand = cand < i ? cand : i;
+    uint32_t age = 0xFFFFFFFFu;  // n - 1 - entry in slot l
+    if (l < dcap && resident) {
+        const uint32_t a = (n - 1u - l) % dcap;
+        if (a < resident && t.rh == h && t.rl == na) age = a;
     }
-    cand = ~wave_max_u32(~cand);  // wave minimum
-    if (lane_id() == 0) sh->red[wave_id()] = cand;
-    __syncthreads();
-    uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-    for (int w = 0; w < TM_NWAVES; w++) best = sh->red[w] < best ? sh->red[w] : best;
-    __syncthreads();
-    if (best != 0xFFFFFFFFu) {
-        const uint16_t* old = b.fx_dlog + (s * dcap + (n - 1u - best) % dcap) * mac;
+    age = ~wave_max_u32(~age);  // the minimum: the newest entry
+    if (age != 0xFFFFFFFFu) {
+        const uint16_t* old = b.fx_dlog + ((size_t)t.s * dcap + (n - 1u - age) % dcap) * stride;
         uint32_t diff = 0;
         for (uint32_t k = threadIdx.x; k < na; k += TM_NT) diff |= old[k] != cells[k] ? 1u : 0u;
-        if (wg_sum(sh, diff) == 0) {
-            if (threadIdx.x == 0) sh->bytes += 2ull * na + 8ull * resident;
+        if (wg_sum1(t, diff) == 0) {
+            if (threadIdx.x == 0) sh->bytes += 2ull * na;
             return true;  // the same set is logged already
         }
     }
-    if (n - f >= dcap) return false;
-    const size_t slot = s * dcap + n % dcap;
-    uint16_t* dst = b.fx_dlog + slot * mac;
+    if (n - t.df >= dcap) return false;
+    const uint32_t sl = n % dcap;
+    const size_t slot = (size_t)t.s * dcap + sl;
+    uint16_t* dst = b.fx_dlog + slot * stride;
     for (uint32_t k = threadIdx.x; k < na; k += TM_NT) dst[k] = cells[k];
     if (threadIdx.x == 0) {
         b.fx_dlen[slot] = (uint16_t)na;
         b.fx_dhash[slot] = h;
-        b.fx_dn[s] = n + 1u;
-        sh->bytes += 2ull * na + 8ull * resident + 8ull;
+        sh->bytes += 2ull * na + 6ull;
     }
-    __syncthreads();
+    if (l == sl) {
+        t.rh = h;
+        t.rl = na;
+    }
+    t.dn = n + 1u;
     return true;
 }
 
@@ -1206,7 +1228,9 @@ __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
     }
     wg_clear(t.infP, t.c.cw);
     wg_clear(reinterpret_cast<uint32_t*>(t.colconf), t.c.ncol);
-    __syncthreads();
+    // (frozen: collect_frozen's cell listing ends with a barrier before any
+    // infP / colConfidence write or qn read)
+    if (!FROZEN) __syncthreads();
     if (FROZEN && t.defer && need != P2_KEEP && t.np <= (uint32_t)t.c.fx_pcap) {
         // the predicted cells first (pid pass): a phase 2 whose confidences the
         // step discards needs nothing else now -- its segments' one-time
@@ -1274,28 +1298,22 @@ __device__ __forceinline__ const uint16_t* lrn_pat(Tm& t, int k) {
 }
 __device__ __forceinline__ int lrn_len(Tm& t, int k) { return t.sh->lrn_len[(t.sh->lrn_head + k) % HTM_MAXPAT]; }
 
-// _inferBacktrack(activeColumns).  gprevP: infPredictedState(t-1) in HBM
-// when the step's state was loaded from there (first step of a run: the
-// write-back comes only at the end of the step), else null.  The replays
-// overwrite the LDS copy, so that one is the backup; otherwise a scratch
-// copy is kept.  NuPIC's saved candidate state is not copied: the loop stops
-// at the candidate, so the live state already is it; and with no candidate
-// the current pattern's phase 1 is recomputed from infP(t-1) instead of
-// restoring a saved infActiveState (same state, computed the same way).
+// _inferBacktrack(activeColumns).  NuPIC copies infPredictedState t -> t-1
+// before every replay's phase 1 and restores t-1 from a backup afterwards;
+// here a replay's phase 1 reads the previous replay's infP directly (its
+// phase 2 clears infP only after phase 1's barriers), so infP(t-1) (infP1) is
+// never touched and needs no backup.  NuPIC's saved candidate state is not
+// copied: the loop stops at the candidate, so the live state already is it;
+// and with no candidate the current pattern's phase 1 is recomputed from
+// infP(t-1) instead of restoring a saved infActiveState (same state,
+// computed the same way).
 template <bool FROZEN>
-__device__ __forceinline__ void infer_backtrack(Tm& t, const uint32_t* gprevP) {
+__device__ __forceinline__ void infer_backtrack(Tm& t) {
     TmSh* sh = t.sh;
-    const int cw = t.c.cw;
     const int numPrev = sh->n_inf_pat;
     if (numPrev <= 0) return;
     const int cur = numPrev - 1;
     if (threadIdx.x == 0) sh->st[1]++;
-    const uint32_t* bkP = gprevP;
-    if (!bkP) {
-        wg_copy(t.sbm + cw, t.infP1, cw);
-        bkP = t.sbm + cw;
-    }
-    __syncthreads();
     uint32_t bad = 0;
     bool haveCand = false;
     int candStart = -1;
@@ -1303,10 +1321,8 @@ __device__ __forceinline__ void infer_backtrack(Tm& t, const uint32_t* gprevP) {
         if (start == cur && haveCand) break;
         bool inSeq = false;
         for (int off = start; off < numPrev; off++) {
-            wg_copy(t.infP1, t.infP, cw);
-            __syncthreads();
             STAMP(t, SB_BT);
-            inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start);
+            inSeq = infer_phase1(t, inf_pat(t, off), inf_len(t, off), off == start, t.infP);
             if (!inSeq) break;
             inSeq = infer_phase2<FROZEN>(t, off == cur ? P2_IF_IN_SEQ : P2_DISCARD);
             if (!inSeq) break;
@@ -1319,8 +1335,6 @@ __device__ __forceinline__ void infer_backtrack(Tm& t, const uint32_t* gprevP) {
         candStart = start;
         break;
     }
-    wg_copy(t.infP1, bkP, cw);
-    __syncthreads();
     if (!haveCand) {
         (void)infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
         (void)infer_phase2<FROZEN>(t);
@@ -1333,15 +1347,13 @@ __device__ __forceinline__ void infer_backtrack(Tm& t, const uint32_t* gprevP) {
         }
         sh->inf_head = (sh->inf_head + npop) % HTM_MAXPAT;
         sh->n_inf_pat -= npop;
-        // infP(t-1) backup: scratch out + in, or one read of the HBM state
-        sh->bytes += (gprevP ? 4ull : 8ull) * cw;
     }
     STAMP(t, SB_BT);
 }
 
 // _updateInferenceState(activeColumns)
 template <bool FROZEN>
-__device__ __forceinline__ void update_inference(Tm& t, const uint32_t* gprevP) {
+__device__ __forceinline__ void update_inference(Tm& t) {
     TmSh* sh = t.sh;
     if (threadIdx.x == 0) {
         if (t.c.max_inf_bt > 0) {
@@ -1363,12 +1375,12 @@ __device__ __forceinline__ void update_inference(Tm& t, const uint32_t* gprevP) 
     __syncthreads();
     bool inSeq = infer_phase1(t, sh->act, sh->nA, sh->reset != 0);
     if (!inSeq) {
-        infer_backtrack<FROZEN>(t, gprevP);
+        infer_backtrack<FROZEN>(t);
         return;
     }
     // with a pattern history, a phase 2 out of sequence is redone by the backtrack
     inSeq = infer_phase2<FROZEN>(t, sh->n_inf_pat > 0 ? P2_IF_IN_SEQ : P2_KEEP);
-    if (!inSeq) infer_backtrack<FROZEN>(t, gprevP);
+    if (!inSeq) infer_backtrack<FROZEN>(t);
 }
 
 // ---------------------------------------------------------------------------
@@ -2082,6 +2094,10 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     }
     t.tb = &b;
     t.defer = FROZEN && b.fx_dlog != nullptr;
+    t.dn = t.df = 0;
+    t.rh = t.rl = 0;
+    t.nsum = 0;
+    if (threadIdx.x == 0) t.sh->acc[0] = t.sh->acc[1] = t.sh->acc[2] = 0u;  // (a barrier follows before any use)
 }
 
 // Write the inference state back to HBM without reading anything: the
@@ -2159,6 +2175,8 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         for (int k = 0; k < HTM_NSTAMP; k++) sh->st_acc[k] = sh->st_cnt[k] = 0;
         sh->st_last = __builtin_amdgcn_s_memtime();
         sh->st_start = sh->st_last;
+        if (sh->st_sp0 && sh->st_sp0 < sh->st_last) sh->st_acc[SB_SP] = sh->st_last - sh->st_sp0;  // the fused SP
+        sh->st_sp0 = 0;
     }
 #endif
     htm_tm_header* hdr = b.hdr + s;
@@ -2242,6 +2260,15 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
             }
         }
         if (threadIdx.x < (uint32_t)c.nw) t.flags[threadIdx.x] = gnzr[threadIdx.x];
+        if (t.defer) {  // the deferred log's counters (every thread keeps a copy) and ring metadata
+            t.dn = b.fx_dn[s];
+            t.df = b.fx_dflushed[s];
+            const uint32_t l = lane_id();
+            if (l < (uint32_t)c.fx_dcap) {
+                t.rh = b.fx_dhash[(size_t)s * c.fx_dcap + l];
+                t.rl = b.fx_dlen[(size_t)s * c.fx_dcap + l];
+            }
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             // header in/out, active list, pattern ring(s), bitmaps in (t-1), the
@@ -2282,7 +2309,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     STAMP(t, SB_LOAD);
     if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) compact_pool(t);
     // ---- BacktrackingTM.compute(input, learn, infer=True)
-    update_inference<FROZEN>(t, first ? gbm + c.cw : nullptr);
+    update_inference<FROZEN>(t);
     STAMP(t, SB_BT);
     if (LEARN) update_learning(t);
     STAMP(t, SB_LEARN);
@@ -2302,17 +2329,21 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
             int hb = 0;
             while (x && hb < 8) { hb++; x >>= 1; }
             sh->st_cnt[SC_HIST + hb] += 1;
-            uint64_t* d = b.dbg + (size_t)s * 2 * HTM_NSTAMP;
+            uint64_t* d = b.dbg + (size_t)s * 4 * HTM_NSTAMP;
+            const bool tail = sh->st_last - sh->st_start >= (1ull << 18);
             for (int k = 0; k < HTM_NSTAMP; k++) {
                 d[k] += sh->st_acc[k];
                 d[HTM_NSTAMP + k] += sh->st_cnt[k];
+                if (tail) {
+                    d[2 * HTM_NSTAMP + k] += sh->st_acc[k];
+                    d[3 * HTM_NSTAMP + k] += sh->st_cnt[k];
+                }
             }
         }
 #endif
         return;
     }
-    // cell bitmaps: only the words that changed.  infA's previous words are
-    // re-read from HBM; on the first step of a run infP1 holds what HBM holds
+    // cell bitmaps whole, colConfidence packed (no reads)
     uint32_t wb = write_back_inference(t, gbm, gval, b.colnz + (size_t)s * (c.nw + 1));
     if (LEARN) {
         wg_copy(gbm + 2 * c.cw, t.lrnA, c.cw);
@@ -2355,6 +2386,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         if (LEARN && (!first || (int)threadIdx.x == sh->ti[1])) hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
     }
     if (threadIdx.x == 0) {
+        if (t.defer) b.fx_dn[s] = t.dn;
         hdr->avg_input_density = sh->avg_dens;
         hdr->avg_learned_seq_length = sh->avg_lsl;
         hdr->lrn_iter = sh->lrn_iter;
@@ -2389,10 +2421,15 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         sh->st_cnt[SC_HIST + hb] += 1;
     }
     if (threadIdx.x == 0 && b.dbg) {
-        uint64_t* d = b.dbg + (size_t)s * 2 * HTM_NSTAMP;
+        uint64_t* d = b.dbg + (size_t)s * 4 * HTM_NSTAMP;
+        const bool tail = sh->st_last - sh->st_start >= (1ull << 18);
         for (int k = 0; k < HTM_NSTAMP; k++) {
             d[k] += sh->st_acc[k];
             d[HTM_NSTAMP + k] += sh->st_cnt[k];
+            if (tail) {
+                d[2 * HTM_NSTAMP + k] += sh->st_acc[k];
+                d[3 * HTM_NSTAMP + k] += sh->st_cnt[k];
+            }
         }
     }
 #endif
@@ -2473,6 +2510,9 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
         }
         const double* v = values + (size_t)k * c.n_streams * c.n_fields;
         const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? sp.enc_in + (size_t)k * c.n_streams * ENC_LIST : nullptr;
+#ifdef HTM_STAMPS
+        if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
+#endif
         if (SPL && sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, bkey, enc);
         else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc);
         __syncthreads();

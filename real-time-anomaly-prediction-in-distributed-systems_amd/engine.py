@@ -272,15 +272,21 @@ class HTMEngine:
         return {k: int(v) for k, v in zip(keys, out)}
 
     def debug_stamps(self) -> dict:
-        """Per-phase TM cycle stamps + event counts (diagnostic stamps build only)."""
-        out = (ctypes.c_uint64 * 48)()
+        """Per-phase TM cycle stamps + event counts (diagnostic stamps build only);
+        "tail": the same over stream-steps whose TM part took >= 2^18 cycles."""
+        out = (ctypes.c_uint64 * 96)()
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
-                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer"]
+                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp"]
         cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
-        return dict(cycles={k: int(out[i]) for i, k in enumerate(names)},
-                    counts={k: int(out[24 + i]) for i, k in enumerate(cnames)},
-                    step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[31 + b]) for b in range(9)})
+
+        def part(o):
+            return dict(cycles={k: int(out[o + i]) for i, k in enumerate(names)},
+                        counts={k: int(out[o + 24 + i]) for i, k in enumerate(cnames)},
+                        step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[o + 31 + b]) for b in range(9)})
+        r = part(0)
+        r["tail"] = part(48)
+        return r
 
     def frozen_index_valid(self) -> bool:
         return bool(self._L.htm_frozen_index_valid(self.h))

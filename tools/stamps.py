@@ -40,4 +40,10 @@ out = {"streams": N, "steps": T, "tm_ms_per_launch": prof["tm_ms"] / prof["steps
        "total_cycles_per_stream_step": round(tot / steps, 1),
        "counts_per_stream_step": {k: round(v / steps, 3) for k, v in st["counts"].items()},
        "step_cycle_hist": st["step_cycle_hist"]}
+tl = st["tail"]
+ts = max(1, tl["counts"]["steps"])
+out["tail"] = {"steps": tl["counts"]["steps"],
+               "cycles_per_stream_step": {k: round(v / ts, 1) for k, v in tl["cycles"].items()},
+               "total_cycles_per_stream_step": round(sum(tl["cycles"].values()) / ts, 1),
+               "counts_per_stream_step": {k: round(v / ts, 3) for k, v in tl["counts"].items()}}
 print(json.dumps(out, indent=1))
