@@ -337,6 +337,14 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // 64 entries flushed every 32 steps 0.273 ms/step, 32 / 16 0.276, 16 / 8 0.304
     d.fx_dcap = n <= 16384 ? 64 : 8;
     if (const char* env = ab_knob("HTM_DEFER_CAP")) d.fx_dcap = std::min(64, std::max(1, std::atoi(env)));  // A/B knob (the flush's job builder handles <= 64)
+    // the ranked phase-2 tail keeps a u16 column and a f32 dutyCycle per
+    // qualifying segment in the union region (free once the counting is
+    // done): bursting steps (~1,500-2,000 qualifying segments on config 2) stay
+    // in LDS instead of taking the HBM-scratch path
+    {
+        const size_t uw = (tm_step_lds_bytes(d, 0, 1) - tm_step_lds_base(d, 0, 1)) / 4;
+        d.q_lds_fx = (int32_t)(uw * 2 / 3 / 64 * 64);
+    }
     return HTM_OK;
 }
 

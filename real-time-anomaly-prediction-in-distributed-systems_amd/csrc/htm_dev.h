@@ -63,6 +63,8 @@ struct DevCfg {
     int32_t fx_pcap;                      // frozen index: max predictive-capable segments (pid space)
     int32_t fx_noff;                      // fx_off entries per stream: ncells*fx_nwin + ncells + 1
     int32_t q_lds;                        // qualifying segments sorted in LDS (more: global path)
+    int32_t q_lds_fx;                     // ... of a frozen phase 2 ranked in LDS (column u16 + dutyCycle f32
+                                          // in the whole union region; more: the HBM scratch)
     int32_t fin_mode;                     // phase-2 tail: 0 column buckets (scans over all columns),
                                           // 1 bitonic key sort, 2 buckets over the nonzero-column bitmap
     int32_t max_act_cells;                // num_desired * K (frozen collection cell list)
@@ -314,21 +316,6 @@ __device__ __forceinline__ void bm_or_field(uint32_t* bm, uint32_t lo, uint32_t 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint32_t t = __shfl_xor(v, o, 64);
-        v = t > v ? t : v;
-    }
-    return v;
-}
-
 // inclusive prefix sum over the wave with DPP (no LDS traffic): Hillis-
 // Steele within each 16-lane row (row_shr 1/2/4/8), then the row totals
 // carried across rows with row_bcast:15 / row_bcast:31 (gfx9 DPP).  Lanes a
@@ -354,6 +341,31 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 #endif
+
+// the value of lane 63 (uniform: a scalar register)
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+// sum / max over the wave (all 64 lanes active): a DPP scan and lane 63's
+// result -- no LDS round trips (a __shfl_xor butterfly is six ds_bpermute's)
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) { return lane63(wave_incl_scan(v)); }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    // lanes a DPP move does not reach take `old` = 0, neutral for unsigned max
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    v = t > v ? t : v;
+    return lane63(v);
+}
 
 // number of set bits of a 64-bit ballot below this lane
 __device__ __forceinline__ uint32_t ballot_rank(uint64_t ball) {

@@ -3,6 +3,8 @@
 // step/run kernels (tm.hip).  See sp.hip for the reference citations and
 // the MI355X design notes.
 #pragma once
+#include <type_traits>
+
 #include "htm_dev.h"
 
 // ScalarEncoder._getFirstOnBit (double arithmetic, NaN -> missing)
@@ -89,17 +91,38 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     for (int k = 0; k < NPL; k++) { p0[k] = 0; p1[k] = 0; }
     const uint32_t* connT = b.connT + (size_t)model_stream(c, s) * c.nin_pad * nw;
     // bit-sliced add of each active input's connected-column row
-    sh.each_active_input(c, [&](int input) {
-        const uint32_t* row = connT + (size_t)input * nw;
-        uint32_t x0 = l < nw ? row[l] : 0u;
-        uint32_t x1 = (l + 64) < nw ? row[l + 64] : 0u;
+    auto add_row = [&](uint32_t x0, uint32_t x1) {
 #pragma unroll
         for (int k = 0; k < NPL; k++) {
             uint32_t t0 = p0[k] & x0, t1 = p1[k] & x1;
             p0[k] ^= x0; p1[k] ^= x1;
             x0 = t0; x1 = t1;
         }
-    });
+    };
+    if constexpr (std::is_same<SH, SpShared>::value) {
+        // the listed inputs' rows, eight loaded before any is added (one HBM
+        // round trip per eight rows instead of one per row; a zero row adds
+        // nothing)
+        constexpr int RB = 8;
+        const int na = sh.n_act_inputs;
+        for (int a0 = 0; a0 < na; a0 += RB) {
+            uint32_t r0[RB], r1[RB];
+#pragma unroll
+            for (int u = 0; u < RB; u++) {
+                const bool in = a0 + u < na;
+                const uint32_t* row = connT + (size_t)(in ? sh.act_inputs[a0 + u] : 0) * nw;
+                r0[u] = in && l < nw ? row[l] : 0u;
+                r1[u] = in && (l + 64) < nw ? row[l + 64] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < RB; u++) add_row(r0[u], r1[u]);
+        }
+    } else {
+        sh.each_active_input(c, [&](int input) {
+            const uint32_t* row = connT + (size_t)input * nw;
+            add_row(l < nw ? row[l] : 0u, (l + 64) < nw ? row[l + 64] : 0u);
+        });
+    }
     // eligibility: overlap >= stimulusThreshold (bit-sliced compare)
     uint32_t gt0 = 0, gt1 = 0, eq0 = ~0u, eq1 = ~0u;
     for (int k = NPL - 1; k >= 0; k--) {
@@ -182,9 +205,9 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     uint32_t pc0 = __popc(cand0), pc1 = __popc(cand1);
     // suffix sum over words > w: total over all - inclusive prefix
     uint32_t incl1 = wave_incl_scan(pc1);
-    uint32_t tot1 = __shfl(incl1, 63, 64);
+    uint32_t tot1 = lane63(incl1);
     uint32_t incl0 = wave_incl_scan(pc0);
-    uint32_t tot0 = __shfl(incl0, 63, 64);
+    uint32_t tot0 = lane63(incl0);
     uint32_t above1 = tot1 - incl1;            // words l+65.. in the upper half
     uint32_t above0 = tot1 + (tot0 - incl0);   // whole upper half + words l+1..63
     // take = clamp(need - above, 0, popcount) in signed arithmetic
@@ -204,13 +227,13 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
     // ascending active list
     uint32_t q0 = __popc(a0), q1 = __popc(a1);
     uint32_t e0 = wave_incl_scan(q0) - q0;
-    uint32_t t0 = __shfl(e0 + q0, 63, 64);
+    uint32_t t0 = lane63(e0 + q0);
     uint32_t e1 = t0 + wave_incl_scan(q1) - q1;
     uint32_t pos = e0;
     for (uint32_t x = a0; x; x &= x - 1) { if (pos < HTM_MAXACT) sh.actlist[pos] = (uint16_t)(l * 32 + __ffs(x) - 1); pos++; }
     pos = e1;
     for (uint32_t x = a1; x; x &= x - 1) { if (pos < HTM_MAXACT) sh.actlist[pos] = (uint16_t)((l + 64) * 32 + __ffs(x) - 1); pos++; }
-    uint32_t total = __shfl(e1 + q1, 63, 64);
+    uint32_t total = lane63(e1 + q1);
     if (l == 0) sh.nact = (int32_t)total;
     if (write_overlaps) {
         int32_t* ov = b.overlaps + (size_t)s * c.ncol;
@@ -467,7 +490,7 @@ __device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b
             if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
             r++;
         }
-        rank_base += __shfl(incl, 63, 64);
+        rank_base += lane63(incl);
     }
 }
 

@@ -591,7 +591,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
                 if (pos < mac) cells[pos] = (uint16_t)(col * (uint32_t)K + (uint32_t)(__ffs(x) - 1));
                 pos++;
             }
-            const uint32_t tot = __shfl(incl, 63, 64);
+            const uint32_t tot = lane63(incl);
             if (a == 0) sh->fx_na = (int32_t)(tot < mac ? tot : mac);
         }
         __syncthreads();
@@ -728,36 +728,56 @@ __device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
     // frozen: the cells the pid counters did not predict (more pids than
     // fx_pcap) come from the segments' synapse rows
     const bool rows = FROZEN && t.np > (uint32_t)c.fx_pcap;
-    for (uint32_t k = threadIdx.x; k < qn && FROZEN; k += TM_NT) {
-        // frozen index: cell and the (frozen-iteration) dutyCycle of the
-        // segment of rank q1[k].  The dutyCycle() state update is a store of
-        // the value it returns; the value read never comes from the pool's
-        // record, which streams sharing a model (fleet) may be refreshing.
-        const uint32_t rank = t.q1[k];
-        const uint2 rec = t.fxrec[rank];
-        const uint32_t cell = rec.x & 0xFFFFu;
-        // the dutyCycle() state write stores the same value every time while
-        // the iteration counter is frozen: only the first one after the index
-        // build changes the record (FX_FRESH marks it done, or never needed)
-        uint32_t slot = ~0u;
-        if (!(rec.x & FX_FRESH) || rows) {
-            slot = t.fxrslot[rank];
-            nb += 4u;
+    // frozen index: cell and the (frozen-iteration) dutyCycle of the segment
+    // of rank q1[k].  Four entries per thread per round: their ranks, then
+    // their records, are loaded before any is used (two round trips per four
+    // instead of two per entry).  The dutyCycle() state update is a store of
+    // the value it returns; the value read never comes from the pool's record,
+    // which streams sharing a model (fleet) may be refreshing.
+    constexpr uint32_t P1B = 4;
+    for (uint32_t k0 = threadIdx.x; k0 < qn && FROZEN; k0 += P1B * TM_NT) {
+        uint32_t rk[P1B];
+        uint2 rc[P1B];
+#pragma unroll
+        for (uint32_t u = 0; u < P1B; u++) {
+            const uint32_t k = k0 + u * TM_NT;
+            rk[u] = k < qn ? t.q1[k] : 0u;
         }
-        if (!(rec.x & FX_FRESH)) {
-            t.duty[(size_t)slot * 3 + 1] = rec.y;
-            t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
-            atomicOr(const_cast<uint32_t*>(&t.fxrec[rank].x), FX_FRESH);
+#pragma unroll
+        for (uint32_t u = 0; u < P1B; u++) {
+            const uint32_t k = k0 + u * TM_NT;
+            rc[u] = k < qn ? t.fxrec[rk[u]] : make_uint2(FX_FRESH, 0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < P1B; u++) {
+            const uint32_t k = k0 + u * TM_NT;
+            if (k >= qn) break;
+            const uint32_t rank = rk[u];
+            const uint2 rec = rc[u];
+            const uint32_t cell = rec.x & 0xFFFFu;
+            // the dutyCycle() state write stores the same value every time while
+            // the iteration counter is frozen: only the first one after the index
+            // build changes the record (FX_FRESH marks it done, or never needed)
+            uint32_t slot = ~0u;
+            if (!(rec.x & FX_FRESH) || rows) {
+                slot = t.fxrslot[rank];
+                nb += 4u;
+            }
+            if (!(rec.x & FX_FRESH)) {
+                t.duty[(size_t)slot * 3 + 1] = rec.y;
+                t.duty[(size_t)slot * 3 + 2] = sh->lrn_iter;
+                atomicOr(const_cast<uint32_t*>(&t.fxrec[rank].x), FX_FRESH);
+                nb += 8u;
+            }
             nb += 8u;
+            if (rows) {
+                const uint32_t nsyn = meta_nsyn(t.meta[slot]);
+                if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
+                    atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
+                nb += 4u;
+            }
+            emit(k, rank, cell, __uint_as_float(rec.y));
         }
-        nb += 8u;
-        if (rows) {
-            const uint32_t nsyn = meta_nsyn(t.meta[slot]);
-            if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
-                atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
-            nb += 4u;
-        }
-        emit(k, rank, cell, __uint_as_float(rec.y));
     }
     for (uint32_t k = threadIdx.x; k < qn && !FROZEN; k += TM_NT) {
         // learning scan: pool slots
@@ -868,7 +888,7 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const uint32_t qn = (uint32_t)sh->qn;
-    const uint32_t ql = (uint32_t)c.q_lds;
+    const uint32_t ql = (uint32_t)c.q_lds_fx;
     const bool in_lds = qn <= ql;
     uint16_t* lcol = reinterpret_cast<uint16_t*>(t.U);  // [ql]
     float* ldc = reinterpret_cast<float*>(t.U + (ql + 1) / 2);  // [ql]
@@ -891,31 +911,50 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
     COUNT(t, SC_P2, 1);
     auto col_at = [&](uint32_t k) -> uint32_t { return in_lds ? (uint32_t)lcol[k] : gcol[k]; };
     auto dc_at = [&](uint32_t k) -> float { return in_lds ? ldc[k] : gdc[k]; };
-    // run heads sum their column in list order
+    // run heads sum their column in list order, four entries loaded at a time
+    // (the adds stay sequential: NuPIC's float order)
     for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
         const uint32_t col = col_at(k);
         if (k > 0 && col_at(k - 1) == col) continue;
         float sum = 0.0f;
-        for (uint32_t j = k; j < qn && col_at(j) == col; j++) sum += dc_at(j);
+        for (uint32_t j = k;; j += 4) {
+            uint32_t cc[4];
+            float dd[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool in = j + u < qn;
+                cc[u] = in ? col_at(j + u) : 0xFFFFFFFFu;
+                dd[u] = in ? dc_at(j + u) : 0.0f;
+            }
+            bool stop = false;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (!stop && cc[u] == col) sum += dd[u];
+                else stop = true;
+            }
+            if (stop) break;
+        }
         t.colconf[col] = sum;
     }
     __syncthreads();
     STAMP(t, SB_SUMS);
     // normaliser: sequential over the columns with a qualifying segment,
     // ascending (= run-head order); wave 0 loads 64 entries at a time and
-    // folds them lane by lane, non-heads adding +0.0f (the sum is unchanged)
+    // folds the run heads among them lane by lane (a ballot names them)
     if (wave_id() == 0) {
         float tot = 0.0f;
         for (uint32_t base = 0; base < qn; base += 64) {
             const uint32_t i = base + lane_id();
             float v = 0.0f;
+            bool head = false;
             if (i < qn) {
                 const uint32_t col = col_at(i);
-                if (i == 0 || col_at(i - 1) != col) v = t.colconf[col];
+                head = i == 0 || col_at(i - 1) != col;
+                if (head) v = t.colconf[col];
             }
             const int vi = __float_as_int(v);
-#pragma unroll
-            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
+            for (uint64_t m = __ballot(head); m; m &= m - 1)
+                tot += __int_as_float(__builtin_amdgcn_readlane(vi, (int)__builtin_ctzll(m)));
         }
         if (lane_id() == 0) sh->tf[0] = tot;
     }
@@ -1002,8 +1041,8 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
                     zo++;
                     off += n;
                 }
-                zbase += __shfl(iz, 63, 64);
-                obase += __shfl(is, 63, 64);
+                zbase += lane63(iz);
+                obase += lane63(is);
             }
             if (l == 0) {
                 nzstart[zbase] = obase;
