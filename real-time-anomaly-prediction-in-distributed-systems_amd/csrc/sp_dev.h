@@ -80,9 +80,56 @@ __device__ __forceinline__ uint32_t bkey_at(const DevCfg& c, int col) {
     return (uint32_t)((col & 31) * (c.nw + 1) + (col >> 5));
 }
 
+// Partial overlaps of the SpShared path by every wave of the workgroup:
+// wave w adds the rows of listed inputs w, w + NW, ... (all of them loaded
+// before any is added: one HBM round trip per wave) into its own bit-sliced
+// planes and stores them to `planes` ([NW][HTM_NPLANES][128] words, LDS);
+// sp_overlap_inhibit's wave 0 then sums the NW partials.  Call with every
+// thread; a barrier must follow.
+constexpr int SP_PLANE_WORDS = 4 * HTM_NPLANES * 128;  // (workgroups of <= 4 waves)
+__device__ __forceinline__ void sp_overlap_partial(const DevCfg& c, const SpBufs& b, int s, const SpShared& sh,
+                                                   uint32_t* planes) {
+    constexpr int NPL = HTM_NPLANES;
+    constexpr int RB = 8;
+    const int l = lane_id(), w = wave_id(), nwv = blockDim.x >> 6;
+    const int nw = c.nw;
+    const uint32_t* connT = b.connT + (size_t)model_stream(c, s) * c.nin_pad * nw;
+    uint32_t p0[NPL], p1[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; k++) { p0[k] = 0; p1[k] = 0; }
+    const int na = sh.n_act_inputs;
+    for (int a0 = w; a0 < na; a0 += RB * nwv) {
+        uint32_t r0[RB], r1[RB];
+#pragma unroll
+        for (int u = 0; u < RB; u++) {
+            const int a = a0 + u * nwv;
+            const bool in = a < na;
+            const uint32_t* row = connT + (size_t)(in ? sh.act_inputs[a] : 0) * nw;
+            r0[u] = in && l < nw ? row[l] : 0u;
+            r1[u] = in && (l + 64) < nw ? row[l + 64] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < RB; u++) {
+            uint32_t x0 = r0[u], x1 = r1[u];
+#pragma unroll
+            for (int k = 0; k < NPL; k++) {
+                uint32_t t0 = p0[k] & x0, t1 = p1[k] & x1;
+                p0[k] ^= x0; p1[k] ^= x1;
+                x0 = t0; x1 = t1;
+            }
+        }
+    }
+    uint32_t* mine = planes + w * NPL * 128;
+#pragma unroll
+    for (int k = 0; k < NPL; k++) {
+        mine[k * 128 + l] = p0[k];
+        mine[k * 128 + 64 + l] = p1[k];
+    }
+}
+
 template <class SH>
 __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs& b, int s, SH& sh, int write_overlaps,
-                                                   uint32_t* bkey = nullptr) {
+                                                   uint32_t* bkey = nullptr, const uint32_t* planes = nullptr) {
     constexpr int NPL = SH::kPlanes;
     const int l = lane_id();
     const int nw = c.nw;
@@ -99,7 +146,30 @@ __device__ __forceinline__ void sp_overlap_inhibit(const DevCfg& c, const SpBufs
             x0 = t0; x1 = t1;
         }
     };
-    if constexpr (std::is_same<SH, SpShared>::value) {
+    if (planes) {
+        // the waves' partial planes (sp_overlap_partial): wave 0's, then the
+        // others added plane by plane (a partial's plane k carries in at bit k;
+        // overlaps stay <= 127, so nothing carries past the top plane)
+        const int nwv = blockDim.x >> 6;
+#pragma unroll
+        for (int k = 0; k < NPL; k++) {
+            p0[k] = planes[k * 128 + l];
+            p1[k] = planes[k * 128 + 64 + l];
+        }
+        for (int w = 1; w < nwv; w++) {
+            const uint32_t* pw = planes + w * NPL * 128;
+#pragma unroll
+            for (int k = 0; k < NPL; k++) {
+                uint32_t x0 = pw[k * 128 + l], x1 = pw[k * 128 + 64 + l];
+#pragma unroll
+                for (int j = k; j < NPL; j++) {
+                    uint32_t t0 = p0[j] & x0, t1 = p1[j] & x1;
+                    p0[j] ^= x0; p1[j] ^= x1;
+                    x0 = t0; x1 = t1;
+                }
+            }
+        }
+    } else if constexpr (std::is_same<SH, SpShared>::value) {
         // the listed inputs' rows, eight loaded before any is added (one HBM
         // round trip per eight rows instead of one per row; a zero row adds
         // nothing)
@@ -559,10 +629,12 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
 // never run paged engines: the frozen-inference bench kernel).
 // bkey: LDS for the boosted inhibition, (nw + 1) * 32 words (used when
 // learning with boostStrength != 0); enc: RDSE engines' encoded lists of the step.
+// planes: LDS for the waves' partial overlaps (SP_PLANE_WORDS; SpShared input
+// only), or null for the one-wave overlap.
 template <bool LEARN, bool PAGED_OK = true, class SH, class IN>
 __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, const IN* input, int s,
                                              SH& sh, int write_overlaps, uint32_t* bkey = nullptr,
-                                             const uint16_t* enc = nullptr) {
+                                             const uint16_t* enc = nullptr, uint32_t* planes = nullptr) {
     const int t = threadIdx.x;
     const bool boosted = LEARN && bkey && c.sp_boost != 0.0f;
     sp_load_input<LEARN>(c, b, input, s, sh, enc);
@@ -571,7 +643,15 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
         for (int col = t; col < c.ncol; col += blockDim.x) bkey[bkey_at(c, col)] = __float_as_uint(bf[col]);
     }
     __syncthreads();
-    if (t < 64) sp_overlap_inhibit(c, b, s, sh, write_overlaps, boosted ? bkey : nullptr);
+    if constexpr (std::is_same<SH, SpShared>::value) {
+        if (planes) {
+            sp_overlap_partial(c, b, s, sh, planes);
+            __syncthreads();
+        }
+    } else {
+        planes = nullptr;
+    }
+    if (t < 64) sp_overlap_inhibit(c, b, s, sh, write_overlaps, boosted ? bkey : nullptr, planes);
     __syncthreads();
     const int nact = sh.nact < HTM_MAXACT ? sh.nact : HTM_MAXACT;
     if (t < nact) b.act[(size_t)s * HTM_MAXACT + t] = sh.actlist[t];

@@ -152,7 +152,7 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
                         : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
     // the fused kernels' SP step, and the boosted-inhibition keys after it
-    size_t spw = align16(sizeof(SpShared)) / 4 + (c.sp_boost != 0.0f ? ((size_t)c.nw + 1) * 32 : 0);
+    size_t spw = align16(sizeof(SpShared)) / 4 + (c.sp_boost != 0.0f ? ((size_t)c.nw + 1) * 32 : 0) + SP_PLANE_WORDS;
     size_t u = fin;
     if (spw > u) u = spw;
     if (keys > u) u = keys;
@@ -2500,6 +2500,9 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
     uint32_t* bkey = c.sp_boost != 0.0f
                          ? reinterpret_cast<uint32_t*>(lds + tm_layout(c, LEARN, FROZEN).off_U + align16(sizeof(SpShared)))
                          : nullptr;
+    // the waves' partial overlaps, past SpShared and the boost keys
+    uint32_t* planes = reinterpret_cast<uint32_t*>(lds + tm_layout(c, LEARN, FROZEN).off_U + align16(sizeof(SpShared))) +
+                       (c.sp_boost != 0.0f ? ((size_t)c.nw + 1) * 32 : 0);
     const uint32_t nblk = (uint32_t)((n_steps + unit_steps - 1) / unit_steps);
     const uint32_t total = (uint32_t)n * nblk;
     // one flat loop over (unit, step) so the compiler sees the same single
@@ -2552,8 +2555,8 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_STAMPS
         if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (SPL && sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, bkey, enc);
-        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc);
+        if (SPL && sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, bkey, enc, planes);
+        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
         __syncthreads();
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
                                     k == k1 - 1);
