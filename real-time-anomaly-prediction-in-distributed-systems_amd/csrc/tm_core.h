@@ -106,7 +106,7 @@ struct Tm {
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER, SB_SP
+    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER, SB_SP, SB_NORM
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -959,6 +959,7 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
         if (lane_id() == 0) sh->tf[0] = tot;
     }
     __syncthreads();
+    STAMP(t, SB_NORM);
     const float tot = sh->tf[0];
     if (tot > 0.0f)
         for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {

@@ -277,7 +277,7 @@ class HTMEngine:
         out = (ctypes.c_uint64 * 96)()
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
-                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp"]
+                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp", "norm"]
         cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
 
         def part(o):
