@@ -8,7 +8,12 @@ from tests/golden/model1_traces.npz).  Inputs are synthetic, resident in HBM:
     cpu[s,t] = clip(trace[(t + 97 s) mod 2324] + d[s,t], 0, 100)
 trace = TestingData.txt cpu column, d uniform integer in {-2..2} from
 numpy PCG64(seed=724).  A step = one network.run(1) of every stream
-(encoder -> SP -> TM -> raw anomaly).  `value` times the K steps in LOCKSTEP
+(encoder -> SP -> TM -> raw anomaly).  Before the W warm-up steps every
+stream replays `--condition` records (default 64, config 2's warm-up in
+SURVEY.md §8(d); one untimed htm_run chunk): the replicated state was trained
+on another part of the trace, and a stream's first steps after meeting its
+own trace position are a bursting transient, not the steady state a
+continuously running stream is in.  `value` times the K steps in LOCKSTEP
 (the headline, north_star's real-time stepping: one htm_step per step, every
 stream advances one record and waits for the slowest); the same engine is
 then timed in run mode (`run_mode`: the K steps as htm_run replay chunks,
@@ -357,6 +362,11 @@ def main():
                          "5: cpu+mem encoders, 4096-column SP, AnomalyLikelihood + SLO harness per record")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: 2324, config 3: 240)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config 2: 64, config 3: 16)")
+    ap.add_argument("--condition", type=int, default=None,
+                    help="configs 2 and 4: records every stream replays (one htm_run chunk, untimed) before the "
+                         "warm-up, so the timed steps see streams in their steady state rather than the transient "
+                         "of a state trained elsewhere meeting a new trace position (SURVEY.md 8(d) config 2's "
+                         "64-step warm-up; default 64, 0 = off)")
     ap.add_argument("--streams", type=int, default=None,
                     help="streams per GPU (config 2: 1024; config 3: 65536, BASELINE.json configs[2])")
     ap.add_argument("--sp-perm-rows", type=int, default=None,
@@ -412,6 +422,8 @@ def main():
         args.chunk = 64 if c4 else 256 if (c3 or c5) else args.steps
     if args.other_steps is None:
         args.other_steps = 0 if c3 else 64 if c4 else 2324
+    if args.condition is None:
+        args.condition = 0 if c3 else 64
     if c4:
         args.chunk = min(args.chunk, int(os.environ.get("HTM_C4_MAX_CHUNK", "64")))
     learn_on = args.config == 2 and not args.no_learn_on and args.shape == "model1"
@@ -471,7 +483,8 @@ def main():
         eng.set_run_chunk(args.chunk)  # one fused launch per htm_run call
     if args.run_unit:
         eng.set_run_unit(args.run_unit)
-    T = args.warmup + args.steps + args.other_steps
+    C = args.condition
+    T = C + args.warmup + args.steps + args.other_steps
     if c4:
         # per-rank jitter stream (a 1M x T matrix per rank would not fit host memory)
         rng = np.random.Generator(np.random.PCG64([724, s0]))
@@ -489,15 +502,17 @@ def main():
                     if args.mode == "run" else
                     torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}"))
 
+    if C:
+        eng.run(vals[:C], out=scores[:C])
     if args.warmup:
-        eng.run(vals[:args.warmup], out=scores[:args.warmup])
+        eng.run(vals[C:C + args.warmup], out=scores[C:C + args.warmup])
     torch.cuda.synchronize()
     dev = f"cuda:{local}"
     c0 = eng.counters()
     if not args.no_profile:
         eng.profile(True)
     # the timed region: K steps bracketed by barrier + synchronize, max over ranks
-    dt, _ = timed_replay(eng, vals, scores, args.warmup, args.steps, args.mode, args.chunk, gather, gathered,
+    dt, _ = timed_replay(eng, vals, scores, C + args.warmup, args.steps, args.mode, args.chunk, gather, gathered,
                          rank, world, dev)
     prof = eng.profile_read() if not args.no_profile else None
     eng.profile(False)
@@ -510,7 +525,7 @@ def main():
         # the other mode on the same engine: run mode (each stream steps through the
         # chunk without waiting for the others) beside the lockstep headline, or back
         omode = "run" if args.mode == "step" else "step"
-        base = args.warmup + args.steps
+        base = C + args.warmup + args.steps
         dl, _ = timed_replay(eng, vals, scores, base, args.other_steps, omode, args.other_steps, None, None,
                              rank, world, dev)
         other = {"mode": omode, "value": round(n_total * args.other_steps / dl, 1), "steps": args.other_steps,
@@ -561,6 +576,7 @@ def main():
                    "mode": ("lockstep: one htm_step (one fused launch) per step, every stream advances one "
                             "network.run(1) per step" if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
+                   "conditioning_steps": C,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
                    "cells_per_column": eng.cells_per_column,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
@@ -616,7 +632,7 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
         child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
                  "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode,
                  "--no-learn-on", "--shape", args.shape]
-        for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows"):
+        for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows", "condition"):
             v = getattr(args, k)
             if v is not None:
                 child += ["--" + k.replace("_", "-"), str(v)]

@@ -889,7 +889,7 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
     TmSh* sh = t.sh;
     const uint32_t qn = (uint32_t)sh->qn;
     const uint32_t ql = (uint32_t)c.q_lds_fx;
-    const bool in_lds = qn <= ql;
+    const bool in_lds = qn + 256u <= ql;  // (the normaliser keeps 256 words past the entries)
     uint16_t* lcol = reinterpret_cast<uint16_t*>(t.U);  // [ql]
     float* ldc = reinterpret_cast<float*>(t.U + (ql + 1) / 2);  // [ql]
     uint32_t* gcol = t.q1;
@@ -939,9 +939,46 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
     __syncthreads();
     STAMP(t, SB_SUMS);
     // normaliser: sequential over the columns with a qualifying segment,
-    // ascending (= run-head order); wave 0 loads 64 entries at a time and
-    // folds the run heads among them lane by lane (a ballot names them)
-    if (wave_id() == 0) {
+    // ascending (= run-head order; zeros in between would add nothing).  In
+    // LDS: every wave takes 64-entry chunks, and the run heads of a chunk write
+    // their column sums, compacted in order, to the chunk's own slots of ldc
+    // (free once the sums are made) with the count in a side array; then wave
+    // 0 folds the chunks in order, each one vector load and `count`
+    // lane-by-lane adds, the next chunk loaded while one is folded.
+    if (in_lds) {
+        float* hv = ldc;
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(ldc + (ql - 256u));
+        const uint32_t nch = (qn + 63u) / 64u;
+        for (uint32_t ch = wave_id(); ch < nch; ch += TM_NWAVES) {
+            const uint32_t i = ch * 64u + lane_id();
+            bool head = false;
+            float v = 0.0f;
+            if (i < qn) {
+                const uint32_t col = lcol[i];
+                head = i == 0 || lcol[i - 1] != col;
+                if (head) v = t.colconf[col];
+            }
+            const uint64_t m = __ballot(head);
+            if (head) hv[ch * 64u + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = v;
+            if (lane_id() == 0) cnt[ch] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        if (wave_id() == 0) {
+            float tot = 0.0f;
+            uint32_t n0 = nch ? cnt[0] : 0u;
+            float v0 = nch ? hv[lane_id()] : 0.0f;
+            for (uint32_t ch = 0; ch < nch; ch++) {
+                const uint32_t n1 = ch + 1 < nch ? cnt[ch + 1] : 0u;
+                const float v1 = ch + 1 < nch ? hv[(ch + 1) * 64u + lane_id()] : 0.0f;
+                const int vi = __float_as_int(v0);
+                const uint32_t nn = __builtin_amdgcn_readfirstlane(n0);
+                for (uint32_t j = 0; j < nn; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, (int)j));
+                n0 = n1;
+                v0 = v1;
+            }
+            if (lane_id() == 0) sh->tf[0] = tot;
+        }
+    } else if (wave_id() == 0) {
         float tot = 0.0f;
         for (uint32_t base = 0; base < qn; base += 64) {
             const uint32_t i = base + lane_id();
