@@ -27,12 +27,17 @@
 #define FX_DEPTH 4                 // frozen index: out-list blocks in flight per thread
 #endif
 #define FX_OWN (FX_DEPTH * TM_NT)  // blocks streamed per pass (block -> list map in LDS)
-// index of the block-list offset of (window w, cell x); FX_CELL_MAJOR (A/B
-// builds only) restores the round-2 [cell][window] order
-#ifdef FX_CELL_MAJOR
-#define FX_LIST(c, w, x) ((size_t)(x) * (c).fx_nwin + (size_t)(w))
+// index of the block-list offset of (list w, cell x): w = -1 the cell's pid
+// list, w >= 0 its rank window w.  Cell-major: a cell's pid list and window
+// lists are one contiguous run of blocks and their offsets are adjacent words,
+// so the passes of a phase 2 after the first find both in cache (same-box A/B
+// vs window-major: same time, HBM traffic 1.99x vs 2.11x the algorithmic
+// bytes, profiles/r03_ab).  FX_WINDOW_MAJOR (A/B builds only) restores the
+// round-3 [window][cell] order.
+#ifdef FX_WINDOW_MAJOR
+#define FX_LIST(c, w, x) ((w) < 0 ? (size_t)(c).ncells * (c).fx_nwin + (size_t)(x) : (size_t)(w) * (c).ncells + (size_t)(x))
 #else
-#define FX_LIST(c, w, x) ((size_t)(w) * (c).ncells + (size_t)(x))
+#define FX_LIST(c, w, x) ((size_t)(x) * ((size_t)(c).fx_nwin + 1) + (size_t)((int)(w) + 1))
 #endif
 #define FX_MAXPER ((HTM_MAXACT * HTM_MAXK + TM_NT - 1) / TM_NT)  // active cells per thread
 
@@ -174,7 +179,7 @@ struct TmBufs {
     // needs of a qualifying segment: its cell and the dutyCycle value it
     // reads while learning is off (the iteration counter is frozen).
     uint64_t* fx_base;      // [S] first block of the stream
-    uint32_t* fx_off;       // [S][fx_noff]: [window][cell] lists, then [cell] pid lists, then the end
+    uint32_t* fx_off;       // [S][fx_noff]: block offsets of the lists in FX_LIST order ([cell][pid, windows]), then the end
     uint4* fx_ent;          // [total blocks] 8 x u16 entries each
     uint2* fx_rec;          // [S][seg_cap] by rank: {cell | FX_FRESH, dutyCycle bits}
     uint32_t* fx_rslot;     // [S][seg_cap] pool slot of each rank

@@ -397,7 +397,7 @@ __device__ void rdse_new_rep(const DevCfg& c, int32_t* h, int16_t* map, int from
 __global__ void rdse_init_kernel(DevCfg c, SpBufs b, int n_streams) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_streams * c.n_fields) return;
-    const int s = t / c.n_fields, f = t % c.n_fields;
+    const int s = t / c.n_fields;  // (field t % n_fields: the block is per (stream, field))
     uint8_t* blk = b.rdse + (size_t)t * c.rdse_block;
     int32_t* h = reinterpret_cast<int32_t*>(blk);
     int16_t* map = reinterpret_cast<int16_t*>(blk + RDSE_HDR_WORDS * 4);

@@ -189,7 +189,6 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
     const uint32_t* conn = b.seg_conn + (size_t)s * sc;
     const uint32_t* rslot = b.fx_rslot + (size_t)s * sc;
     const size_t noff = (size_t)c.fx_noff;
-    const size_t p0 = (size_t)c.ncells * c.fx_nwin;  // first pid-list counter
     uint32_t* off = b.fx_off + (size_t)s * noff;
     uint32_t* pid = b.scr_q2 + (size_t)s * sc;  // by rank
     uint16_t* pcell = b.fx_pcell + (size_t)s * c.fx_pcap;
@@ -208,7 +207,7 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
         const uint32_t m = meta[slot];
         const uint32_t nsyn = meta_nsyn(m), w = r / (uint32_t)c.fx_win;
         for (uint32_t j = 0; j < nsyn; j++)
-            atomicAdd(&off[FX_LIST(c, w, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
+            atomicAdd(&off[FX_LIST(c, (int)w, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
         const uint32_t cm = conn[slot] & (nsyn >= 32 ? ~0u : ((1u << nsyn) - 1u));
         uint32_t p = ~0u;
         if (__popc(cm) >= (uint32_t)c.act_thr) {
@@ -237,7 +236,7 @@ __global__ void tm_fx_count_kernel(DevCfg c, TmBufs b, uint64_t* counts) {
             pcell[next] = (uint16_t)meta_cell(m);
             next++;
             for (uint32_t j = 0; j < nsyn; j++)
-                if ((cm >> j) & 1u) atomicAdd(&off[p0 + src[(size_t)slot * HTM_MAXSYN + j]], 1u);
+                if ((cm >> j) & 1u) atomicAdd(&off[FX_LIST(c, -1, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
         }
     }
     __syncthreads();
@@ -285,7 +284,6 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
     const uint32_t* pid = b.scr_q2 + (size_t)s * sc;
     const uint32_t* rslot = b.fx_rslot + (size_t)s * sc;
     const size_t noff = (size_t)c.fx_noff;
-    const size_t p0 = (size_t)c.ncells * c.fx_nwin;
     const uint32_t* off = b.fx_off + (size_t)s * noff;
     uint32_t* cur = b.scr_cur + (size_t)s * noff;
     uint16_t* ent = reinterpret_cast<uint16_t*>(b.fx_ent + b.fx_base[s]);
@@ -301,7 +299,7 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
         const uint32_t m = meta[slot];
         const uint32_t nsyn = meta_nsyn(m), w = r / W;
         for (uint32_t j = 0; j < nsyn; j++) {
-            uint32_t pos = atomicAdd(&cur[FX_LIST(c, w, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
+            uint32_t pos = atomicAdd(&cur[FX_LIST(c, (int)w, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
             ent[pos] = (uint16_t)(r - w * W);
         }
         // FX_FRESH: the record already holds what a frozen dutyCycle() stores
@@ -313,7 +311,7 @@ __global__ void tm_fx_fill_kernel(DevCfg c, TmBufs b) {
             const uint32_t cm = conn[slot];
             for (uint32_t j = 0; j < nsyn; j++) {
                 if (!((cm >> j) & 1u)) continue;
-                uint32_t pos = atomicAdd(&cur[p0 + src[(size_t)slot * HTM_MAXSYN + j]], 1u);
+                uint32_t pos = atomicAdd(&cur[FX_LIST(c, -1, src[(size_t)slot * HTM_MAXSYN + j])], 1u);
                 ent[pos] = (uint16_t)p;
             }
         }

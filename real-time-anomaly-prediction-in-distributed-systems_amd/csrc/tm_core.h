@@ -604,7 +604,6 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
     const uint32_t nr = t.nr;
     STAMP(t, SB_LIST);
     COUNT(t, SC_NACT, na);
-    const uint32_t nwin = (uint32_t)c.fx_nwin;
     const uint32_t nw = (nr + W - 1) / W;
     const bool pid_ok = t.np <= (uint32_t)c.fx_pcap;
     const uint32_t per = (na + TM_NT - 1) / TM_NT;  // <= FX_MAXPER (na <= 64 x 32)
@@ -616,7 +615,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
     constexpr uint32_t FX_PF = 2;
     uint32_t olo[FX_PF], ohi[FX_PF];
     auto off_idx = [&](int w, uint32_t k) {
-        return w < 0 ? (size_t)c.ncells * nwin + cells[k] : FX_LIST(c, (uint32_t)w, cells[k]);
+        return FX_LIST(c, w, cells[k]);
     };
     auto load_offsets = [&](int w) {
 #pragma unroll
