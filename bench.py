@@ -10,10 +10,12 @@ trace = TestingData.txt cpu column, d uniform integer in {-2..2} from
 numpy PCG64(seed=724).  A step = one network.run(1) of every stream
 (encoder -> SP -> TM -> raw anomaly).  Before the W warm-up steps every
 stream replays `--condition` records (default 64, config 2's warm-up in
-SURVEY.md §8(d); one untimed htm_run chunk): the replicated state was trained
+SURVEY.md §8(d), untimed): the replicated state was trained
 on another part of the trace, and a stream's first steps after meeting its
 own trace position are a bursting transient, not the steady state a
-continuously running stream is in.  `value` times the K steps in LOCKSTEP
+continuously running stream is in (the conditioning and the warm-up run in
+the measured mode: lockstep steps also bring the deferred-duty log, empty
+after replay chunks, to its steady state).  `value` times the K steps in LOCKSTEP
 (the headline, north_star's real-time stepping: one htm_step per step, every
 stream advances one record and waits for the slowest); the same engine is
 then timed in run mode (`run_mode`: the K steps as htm_run replay chunks,
@@ -363,10 +365,10 @@ def main():
     ap.add_argument("--steps", type=int, default=None, help="timed steps (config 2: 2324, config 3: 240)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config 2: 64, config 3: 16)")
     ap.add_argument("--condition", type=int, default=None,
-                    help="configs 2 and 4: records every stream replays (one htm_run chunk, untimed) before the "
-                         "warm-up, so the timed steps see streams in their steady state rather than the transient "
-                         "of a state trained elsewhere meeting a new trace position (SURVEY.md 8(d) config 2's "
-                         "64-step warm-up; default 64, 0 = off)")
+                    help="configs 2 and 4: records every stream steps through (untimed, in the measured mode) "
+                         "before the warm-up, so the timed steps see streams in their steady state rather than "
+                         "the transient of a state trained elsewhere meeting a new trace position (SURVEY.md 8(d) "
+                         "config 2's 64-step warm-up; default 64, 0 = off)")
     ap.add_argument("--streams", type=int, default=None,
                     help="streams per GPU (config 2: 1024; config 3: 65536, BASELINE.json configs[2])")
     ap.add_argument("--sp-perm-rows", type=int, default=None,
@@ -502,10 +504,17 @@ def main():
                     if args.mode == "run" else
                     torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}"))
 
-    if C:
-        eng.run(vals[:C], out=scores[:C])
-    if args.warmup:
-        eng.run(vals[C:C + args.warmup], out=scores[C:C + args.warmup])
+    # conditioning and warm-up in the measured mode: lockstep steps also bring
+    # the deferred-duty log to its steady state (its ring starts empty; the
+    # first lockstep steps after replay chunks log every new active set)
+    for a0, n_ in ((0, C), (C, args.warmup)):
+        if not n_:
+            continue
+        if args.mode == "step":
+            for k in range(a0, a0 + n_):
+                eng.step(vals[k], out=scores[k])
+        else:
+            eng.run(vals[a0:a0 + n_], out=scores[a0:a0 + n_])
     torch.cuda.synchronize()
     dev = f"cuda:{local}"
     c0 = eng.counters()
