@@ -51,7 +51,6 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t ncand;
     int32_t ti[8];
     int32_t npc_known;  // numPredictedCols of the current frozen phase 2 once counted, else -1
-    int32_t colbits_ok; // frozen: t.flags holds the predicted columns of the last pid pass
     int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
     uint32_t p1_off;    // LDS offset of the active columns (ascending) phase 1 built infA from
     int32_t p1_n;       // their number, or -1 when infA is not phase 1's
@@ -507,22 +506,17 @@ __device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t
     const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
     const uint32_t per = (nquads + TM_NT - 1) / TM_NT;  // <= FX_CQ (fx_win <= 64512)
     const uint32_t q0 = threadIdx.x * per;
-    // one sweep: every quad of the thread's run loaded at once; a quad with a
-    // hit only sets a bit (hq) and adds its popcount -- the hits themselves
-    // are read back from LDS after the scan (counters are cleared only after
-    // the next pass's first barrier), so the sweep costs ~12 VALU ops a quad
-    uint32_t hq = 0, mine = 0;
+    // one sweep: every quad of the thread's run loaded at once, its hits kept
+    // as 16-bit masks (two per register)
+    uint32_t hm[FX_CQ / 2];
+    uint32_t mine = 0;
 #pragma unroll
     for (int i = 0; i < FX_CQ; i++) {
-        if ((uint32_t)i < per && q0 + i < nquads) {
-            const uint4 x = c4[q0 + i];
-            const uint32_t a0 = (x.x + add) & 0x80808080u, a1 = (x.y + add) & 0x80808080u;
-            const uint32_t a2 = (x.z + add) & 0x80808080u, a3 = (x.w + add) & 0x80808080u;
-            if (a0 | a1 | a2 | a3) {
-                hq |= 1u << i;
-                mine += __popc(a0) + __popc(a1) + __popc(a2) + __popc(a3);
-            }
-        }
+        uint32_t h = 0;
+        if ((uint32_t)i < per && q0 + i < nquads) h = fx_quad_hits(c4[q0 + i], add);
+        if (i & 1) hm[i >> 1] |= h << 16;
+        else hm[i >> 1] = h;
+        mine += __popc(h);
     }
     // exclusive prefix over the workgroup in thread order (one barrier)
     const uint32_t qn0 = (uint32_t)sh->qn;  // thread 0 updates it only after the barrier
@@ -536,14 +530,11 @@ __device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t
         if (v < (int)wave_id()) pos += x;
         tot += x;
     }
-    for (uint32_t hb = hq; hb; hb &= hb - 1) {
-        const uint32_t i = (uint32_t)__ffs(hb) - 1u;
-        const uint4 x = c4[q0 + i];
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    if (mine) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            for (uint32_t m = (w[j] + add) & 0x80808080u; m; m &= m - 1) {
-                const uint32_t b = 4u * (uint32_t)j + (((uint32_t)__ffs(m) - 1u) >> 3);  // 4 * word + byte
+        for (int i = 0; i < FX_CQ; i++) {
+            for (uint32_t m = (hm[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; m; m &= m - 1) {
+                const uint32_t b = __ffs(m) - 1;  // 4 * word + byte
                 if (pos < qcap) dst[pos] = base + 16 * (q0 + i) + b;
                 pos++;
             }
@@ -677,12 +668,6 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
         const uint32_t span = w < 0 ? t.np : (nr - (uint32_t)w * W < W ? nr - (uint32_t)w * W : W);
         const uint32_t nbytes = (span + 15u) & ~15u;
         wg_clear4(cnt, nbytes / 16);
-        if (w < 0) {
-            // the pid pass also marks the predicted columns (t.flags is free
-            // between the step's anomaly input and its write-back)
-            for (int i = threadIdx.x; i < c.nw; i += TM_NT) t.flags[i] = 0u;
-            if (threadIdx.x == 0) sh->colbits_ok = 1;
-        }
         __syncthreads();
         STAMP(t, SB_WINPRE);
         COUNT(t, SC_WIN, 1);
@@ -695,32 +680,12 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
             const uint32_t np = t.np;
             uint32_t* infP = t.infP;
             const uint16_t* pcell = t.fxpcell;
-            // (the predicted pids of a thread's counter quads are gathered
-            // first, four cell lookups in flight at a time; the predicted
-            // columns are marked in t.flags for count_predicted_cols)
-            const uint32_t add = 0x01010101u * (128u - (uint32_t)c.act_thr);
-            const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
-            for (uint32_t i = threadIdx.x; i < nbytes / 16; i += TM_NT) {
-                const uint4 x = c4[i];
-                const uint32_t hm = fx_quad_hits(x, add);  // bit 4j + b: byte b of word j
-                for (uint32_t m = hm; m;) {
-                    uint32_t pid[4], cl[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        pid[u] = m ? 16u * i + (uint32_t)(__ffs(m) - 1) : 0xFFFFFFFFu;
-                        m &= m - 1;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; u++) cl[u] = pid[u] < np ? pcell[pid[u]] : 0xFFFFFFFFu;
-#pragma unroll
-                    for (int u = 0; u < 4; u++)
-                        if (cl[u] != 0xFFFFFFFFu) {
-                            atomicOr(&infP[cl[u] >> 5], 1u << (cl[u] & 31));
-                            const uint32_t col = col_of(c, cl[u]);
-                            atomicOr(&t.flags[col >> 5], 1u << (col & 31));
-                        }
+            fx_qualify(cnt, nbytes, (uint32_t)c.act_thr, [&](uint32_t pid) {
+                if (pid < np) {
+                    const uint32_t cell = pcell[pid];
+                    atomicOr(&infP[cell >> 5], 1u << (cell & 31));
                 }
-            }
+            });
             __syncthreads();
         }
         STAMP(t, SB_QSCAN);
@@ -831,13 +796,8 @@ __device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
 __device__ __forceinline__ uint32_t count_predicted_cols(Tm& t) {
     const DevCfg& c = t.c;
     uint32_t n = 0;
-    if (t.sh->colbits_ok) {
-        // the pid pass marked them: popcounts of nw <= 128 words
-        for (int i = threadIdx.x; i < c.nw; i += TM_NT) n += __popc(t.flags[i]);
-    } else {
-        for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
-            if (bm_field(t.infP, (uint32_t)col * c.K, c.K)) n++;
-    }
+    for (int col = threadIdx.x; col < c.ncol; col += TM_NT)
+        if (bm_field(t.infP, (uint32_t)col * c.K, c.K)) n++;
     return wg_sum1(t, n);
 }
 
@@ -1341,7 +1301,6 @@ __device__ __forceinline__ bool infer_phase2(Tm& t, int need = P2_KEEP) {
         sh->st[0]++;
         sh->qn = 0;
         sh->npc_known = -1;
-        sh->colbits_ok = 0;
     }
     wg_clear(t.infP, t.c.cw);
     wg_clear(reinterpret_cast<uint32_t*>(t.colconf), t.c.ncol);
