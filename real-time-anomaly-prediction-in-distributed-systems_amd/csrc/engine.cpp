@@ -498,6 +498,12 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (const char* env = ab_knob("HTM_RUN_UNIT")) e->run_unit = std::max(1, std::atoi(env));  // A/B knob
     if (const char* env = ab_knob("HTM_DEFER_DUTY")) e->defer = std::atoi(env) != 0;            // A/B knob
     if (const char* env = ab_knob("HTM_DEFER_FLUSH_EVERY")) e->flush_every = std::max(1, std::atoi(env));  // test knob
+    // fleet-sized engines (8-entry logs, a flush every 4 steps) flush on the
+    // step stream: beside the steps, 131,072-stream fleets ran bimodal (15 or
+    // 30 ms per step) and faulted (illegal address) in some runs; on the step
+    // stream 14.7 ms (Model-1) / 23.5 ms (model.yaml), clean in every run
+    // (profiles/r03_ab/fleet_flush_mode.txt)
+    if (n_streams > 16384) e->flush_mode = 1;
     if (const char* env = ab_knob("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
