@@ -96,3 +96,32 @@ def test_lockstep_test_phase_matches_golden(rt, model1, traces):
     sa, sb = e.tm_segments(0), ref.tm_segments(0)
     for k in ("last_dc", "last_dc_iter", "pos_act"):
         assert np.array_equal(sa[k], sb[k]), k
+
+
+def test_frozen_learn_frozen_cycle(rt, model1, traces):
+    """Deferred writes across a frozen -> TM learning -> frozen cycle: the
+    re-frozen index starts an empty log (engine.cpp build_fx), so an active
+    set logged before the learning phase is not taken for one already written
+    at the new iteration.  Scores, counters and the segment records (dutyCycle
+    cache included) equal the undeferred engine in every phase."""
+    n, T = 32, 48
+    rng = np.random.default_rng(29)
+    test = np.asarray(traces["test"], np.float64)
+    t = np.arange(3 * T)[:, None]
+    s = np.arange(n)[None, :]
+    vals = torch.tensor(np.clip(test[(t + 31 * s) % len(test)] + rng.integers(-2, 3, size=(3 * T, n)), 0, 100),
+                        device="cuda")
+    a = replicas(rt, model1, n)
+    b = replicas(rt, model1, n)
+    b.defer_duty(False)
+    for k, tm_learn in enumerate((False, True, False)):
+        for e in (a, b):
+            e.set_learning(False, tm_learn)
+        ga, gb = lockstep(a, vals[k * T:(k + 1) * T]), lockstep(b, vals[k * T:(k + 1) * T])
+        assert np.array_equal(ga, gb), k
+        for region in ("tm_seg_duty", "tm_seg_meta"):
+            assert np.array_equal(a.export_state(region), b.export_state(region)), (k, region)
+    ca, cb = a.counters(), b.counters()
+    for key in ("inf_phase2", "inf_backtracks", "lrn_phase2", "seg_live", "error"):
+        assert ca[key] == cb[key], key
+    assert ca["inf_backtracks"] > 0
