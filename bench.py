@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "HTM stream-steps/sec (2048-col SP+TM, learn on/off) at 1/2/4/8 GPUs; % HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md, L2 (per XCD): ~34.5 TB/s aggregate
 
 
 def make_inputs(n_total, s0, s1, t0, t1, trace):
@@ -220,6 +221,35 @@ def bench_learn_on(args, rt, trace, world, rank, local, pmc_summary=None, pmc_no
     return rec
 
 
+def launch_ranks(n):
+    """bench.py --gpus N without a launcher: start N ranks of this same command
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) and
+    return their exit status.  Called before this process touches the GPU."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench: launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def bench_build_info(rt):
+    """The optimisation level every unit of the loaded library built at
+    (htm_build_info, csrc/cc.sh).  The bench kernel's unit must be -O3."""
+    info = rt._lib.build_info()
+    if info.get("tm_k_frozen.hip") != "-O3":
+        raise SystemExit(f"bench.py: the bench kernel (tm_k_frozen.hip) was built at {info.get('tm_k_frozen.hip')}, "
+                         "not -O3 (csrc/cc.sh fell back past a gfx950 verifier rejection): refusing to measure it")
+    levels = {k: v for k, v in info.items() if k not in ("compiler", "arch")}
+    return {"all_units_O3": all(v == "-O3" for v in levels.values()), "bench_kernel_unit": "tm_k_frozen.hip -O3",
+            "below_O3": {k: v for k, v in levels.items() if v != "-O3"}, "compiler": info.get("compiler"),
+            "arch": info.get("arch")}
+
+
 def pmc_kernel(path, base):
     pm = json.load(open(path))
     ks = [v for n, v in pm.get("kernels", {}).items()
@@ -356,7 +386,14 @@ def bench_config5(args, rt, d, world, rank, local):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one rank each (default 1).  Without WORLD_SIZE in the environment "
+                         "and N > 1, bench.py launches the N ranks itself (torch.distributed.run, before any GPU "
+                         "call) and exits with their status; under a launcher it must equal WORLD_SIZE")
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="launcher test only (tests/test_bench_launch.py): gloo on the CPU with a deterministic "
+                         "stand-in engine in place of the HIP engine -- exercises the rank launch, sharding, "
+                         "gathers and max-over-ranks timing; its line says so and measures nothing")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="2 (default, the metric's config): trained Model-1 streams, learning off; "
                          "3: fresh streams (seed 2045 + s), SP+TM learning on, 256 steps; "
@@ -383,8 +420,8 @@ def main():
                          "steps as htm_run replay chunks, each stream steps through a chunk without waiting "
                          "for the others (the reference's offline replay of recorded metrics, batched)")
     ap.add_argument("--chunk", type=int, default=None,
-                    help="steps per htm_run call (= per fused launch) in run mode (config 2: all K steps; "
-                         "3, 5: 256; 4: 64)")
+                    help="steps per htm_run call (= per fused launch) in run mode (config 2: 2324, the "
+                         "TestingData replay in one launch, whatever --steps is; 3, 5: 256; 4: 64)")
     ap.add_argument("--run-unit", type=int, default=None, help="engine: steps per work-queue unit (HTM_OPT_RUN_UNIT)")
     ap.add_argument("--other-steps", type=int, default=None,
                     help="after the timed region, also time this many steps in the other mode (run mode "
@@ -400,6 +437,9 @@ def main():
     ap.add_argument("--learn-steps", type=int, default=32, help="learn_on: timed lockstep steps")
     ap.add_argument("--learn-warmup", type=int, default=8, help="learn_on: untimed steps")
     ap.add_argument("--pmc-summary-learn", default=None, help="counter summary of the learn_on leg (see --pmc-summary)")
+    ap.add_argument("--flush-mode", choices=["auto", "0", "1"], default="auto",
+                    help="where the deferred-write flush runs (HTM_OPT_FLUSH_MODE): 0 beside the steps on the "
+                         "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
     ap.add_argument("--shape", choices=["model1", "yaml"], default="model1",
                     help="model1 (default): the reference's Model-1 parameters (12 cells/column); yaml: the "
                          "reference's model.yaml set (RDSE, boostStrength 3, 32 cells/column; configs 2 and 4)")
@@ -421,16 +461,26 @@ def main():
     if args.seg_capacity is None:
         args.seg_capacity = 10240 if c3 else (1 << 17) if args.shape == "yaml" else 72 * 1024
     if args.chunk is None:
-        args.chunk = 64 if c4 else 256 if (c3 or c5) else args.steps
+        args.chunk = 64 if c4 else 256 if (c3 or c5) else 2324
     if args.other_steps is None:
         args.other_steps = 0 if c3 else 64 if c4 else 2324
     if args.condition is None:
         args.condition = 0 if c3 else 64
     if c4:
         args.chunk = min(args.chunk, int(os.environ.get("HTM_C4_MAX_CHUNK", "64")))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and (args.gpus or 1) > 1:
+        # one process per GPU: launch the N ranks (before this process touches
+        # the GPU) and report their status
+        sys.exit(launch_ranks(args.gpus))
+    if world_env is not None and args.gpus is not None and int(world_env) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world_env}")
+    standin = args.cpu_standin
+    if standin:
+        args.no_learn_on = args.no_cpu = args.no_pmc = args.no_profile = True
     learn_on = args.config == 2 and not args.no_learn_on and args.shape == "model1"
     pmc_note = pmc_note_learn = None
-    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_pmc and not c5
+    if (int(world_env or "1") == 1 and not args.no_pmc and not c5
             and not os.environ.get("HTM_BENCH_PMC_CHILD")):
         # before this process touches the GPU: the HBM counter passes, each a
         # short run of this same command under rocprofv3 in a child process
@@ -445,11 +495,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if standin:
+        dev = "cpu"
+        sync = lambda: None  # noqa: E731
+    else:
+        torch.cuda.set_device(local)
+        dev = f"cuda:{local}"
+        sync = torch.cuda.synchronize
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if standin else "nccl")
     import _pkg
     rt = _pkg.load()
+    build = None if standin else bench_build_info(rt)
 
     d = np.load(os.path.join(ROOT, "tests", "golden", "model1_traces.npz"))
     if c5:
@@ -462,13 +519,18 @@ def main():
     s0, s1 = rt.fleet.shard_range(n_total, world, rank)
     # the reference's model.yaml parameter set (RDSE, boosting, 32 cells/column) or Model 1
     shape = dict(rt._lib.MODEL_YAML) if args.shape == "yaml" else {}
-    if c3:
+    if standin:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import bench_standin
+        eng = bench_standin.StandInEngine(S, s0)
+        train_s, hdr, model_dist = 0.0, None, "cpu stand-in (launcher test: no HTM compute)"
+    elif c3:
         # fresh per-stream init (seeds 2045 + global stream index), learning on
         cfg = rt.default_config(seg_capacity=args.seg_capacity, upd_capacity=512, seed_stride=1,
                                 sp_seed=2045 + s0, tm_seed=2045 + s0, sp_perm_rows=args.sp_perm_rows)
         t0 = time.time()
         eng = rt.HTMEngine(S, config=cfg, device=local)
-        torch.cuda.synchronize()
+        sync()
         train_s, hdr, model_dist = time.time() - t0, None, "fresh per-stream init"
         eng.set_learning(True, True)
     elif c4:
@@ -483,6 +545,8 @@ def main():
         eng.set_learning(False, False)
     if not c3:
         eng.set_run_chunk(args.chunk)  # one fused launch per htm_run call
+    if args.flush_mode != "auto" and not standin:
+        eng.flush_mode(int(args.flush_mode))
     if args.run_unit:
         eng.set_run_unit(args.run_unit)
     C = args.condition
@@ -493,16 +557,16 @@ def main():
         t_ = np.arange(T)[:, None]
         g_ = np.arange(s0, s1)[None, :]
         vals = torch.tensor(np.clip(trace[(t_ + 97 * g_) % len(trace)] + rng.integers(-2, 3, size=(T, S)), 0, 100)
-                            .astype(np.float64), device=f"cuda:{local}")
+                            .astype(np.float64), device=dev)
     else:
-        vals = torch.tensor(make_inputs(n_total, s0, s1, 0, T, trace), device=f"cuda:{local}")
-    scores = torch.empty((T, S), dtype=torch.float32, device=f"cuda:{local}")
+        vals = torch.tensor(make_inputs(n_total, s0, s1, 0, T, trace), device=dev)
+    scores = torch.empty((T, S), dtype=torch.float32, device=dev)
     gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
     gathered = None
     if world > 1 and rank == 0:
-        gathered = (torch.empty((world, args.steps, gather.width), dtype=torch.float32, device=f"cuda:{local}")
+        gathered = (torch.empty((world, args.steps, gather.width), dtype=torch.float32, device=dev)
                     if args.mode == "run" else
-                    torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=f"cuda:{local}"))
+                    torch.empty((args.steps, world, gather.width), dtype=torch.float32, device=dev))
 
     # conditioning and warm-up in the measured mode: lockstep steps also bring
     # the deferred-duty log to its steady state (its ring starts empty; the
@@ -515,8 +579,7 @@ def main():
                 eng.step(vals[k], out=scores[k])
         else:
             eng.run(vals[a0:a0 + n_], out=scores[a0:a0 + n_])
-    torch.cuda.synchronize()
-    dev = f"cuda:{local}"
+    sync()
     c0 = eng.counters()
     if not args.no_profile:
         eng.profile(True)
@@ -551,15 +614,11 @@ def main():
         else:   # frozen inference: the kernel's own count of the index blocks and state it moves
             per_launch = (c1["tm_bytes"] - c0["tm_bytes"]) / launches
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = None, pmc_note
+        traffic, tsrc, k = None, pmc_note, None
         if args.pmc_summary:
             # HBM bytes per launch measured by rocprofv3 --pmc passes of THIS command
             # (tools/pmc_summary.py, run in the same gpurun call; corrections there)
-            pm = json.load(open(args.pmc_summary))
-            base = kernel_name(c3, c4, eng.fused)
-            ks = [v for n, v in pm.get("kernels", {}).items()
-                  if n.split("(")[0].replace("void ", "").strip() == base and "hbm_bytes_per_dispatch" in v]
-            k = ks[0] if ks else None
+            k = pmc_kernel(args.pmc_summary, kernel_name(c3, c4, eng.fused))
             if k:
                 traffic = int(k["hbm_bytes_per_dispatch"])
                 tsrc = (f"rocprofv3 --pmc passes of this command ({args.pmc_summary}): {k.get('formula', '')}; "
@@ -571,12 +630,32 @@ def main():
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
                 "bytes_per_launch": int(per_launch),
                 "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
+        if c4:
+            # a fleet's streams share one model: its index and records are read
+            # from the XCD L2s and the Infinity Cache, so the bytes the kernel
+            # requests are not HBM bytes.  frac is the counter-measured HBM
+            # traffic / time; the requested bytes are set against the L2 side
+            # (aggregate L2 bandwidth, MI355X_MICROARCH.md, with the TCC hit rate)
+            req_gbs = achieved
+            hbm_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic else None
+            roof["achieved"] = round(hbm_gbs, 2) if hbm_gbs is not None else None
+            roof["frac"] = round(hbm_gbs / HBM_PEAK_GBS, 5) if hbm_gbs is not None else None
+            roof["frac_basis"] = ("counter HBM bytes per launch / HIP-event launch time" if hbm_gbs is not None else
+                                  "no counters: HBM fraction not measured (requested bytes are L2-served)")
+            l2 = (k or {}).get("l2") or {}
+            roof["l2_side"] = {"requested_gbs": round(req_gbs, 2), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(req_gbs / L2_PEAK_GBS, 5), "tcc_hit_rate": l2.get("hit_rate"),
+                               "tcc_req_per_launch": l2.get("req"),
+                               "basis": "bytes the kernel requests per launch (its own count: index blocks, "
+                                        "records, state) / launch time, against the aggregate L2 bandwidth; "
+                                        "hit rate TCC_HIT/(TCC_HIT+TCC_MISS) from the pmc_l2 pass"}
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "stream-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f32",
-        "data": "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config %d)"
-                % args.config,
+        "data": ("CPU STAND-IN ENGINE (launcher test; no HTM compute, not a measurement)" if standin else
+                 "synthetic: TestingData cpu trace + PCG64(724) jitter, resident in HBM (SURVEY.md §8(d) config %d)"
+                 % args.config),
         "config": {"workload": ("config3: fresh Model-1 streams (seed 2045+s), SP+TM learning on" if c3 else
                                 "config4 fleet: streams sharing one frozen GPU-trained %s SP+TM, "
                                 "per-stream TM state, learn off" % shape_name if c4 else
@@ -585,7 +664,7 @@ def main():
                    "mode": ("lockstep: one htm_step (one fused launch) per step, every stream advances one "
                             "network.run(1) per step" if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
-                   "conditioning_steps": C,
+                   "conditioning_steps": C, "flush_mode": args.flush_mode,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
                    "cells_per_column": eng.cells_per_column,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
@@ -594,7 +673,8 @@ def main():
                                      "device_gb": round(eng.device_bytes() / 1e9, 1)} if c3 else None),
                    ("init_s" if c3 else "train_s"): round(train_s, 2),
                    "model_distribution": model_dist,
-                   "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL gather of scores" if world > 1 else "")},
+                   "parallelism": f"streams sharded over {world} GPU(s)" + (", RCCL gather of scores" if world > 1 else ""),
+                   "build": build},
         "roofline": roof,
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
         ("run_mode" if args.mode == "step" else "lockstep"): other,
@@ -617,6 +697,7 @@ PMC_PASSES = {
     "pmc_fetch": ["FETCH_SIZE"],
     "pmc_wr": ["WRITE_SIZE", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"],
 }
+PMC_L2_PASS = {"pmc_l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum"]}
 
 
 def self_pmc_passes(args, steps=128, learn_leg=False):
@@ -641,12 +722,17 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
         child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
                  "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode,
                  "--no-learn-on", "--shape", args.shape]
+        if args.flush_mode != "auto":
+            child += ["--flush-mode", args.flush_mode]
         for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows", "condition"):
             v = getattr(args, k)
             if v is not None:
                 child += ["--" + k.replace("_", "-"), str(v)]
     env = dict(os.environ, TMPDIR="/tmp", HTM_BENCH_PMC_CHILD="1")
-    for name, counters in PMC_PASSES.items():
+    passes = dict(PMC_PASSES)
+    if args.config == 4 and not learn_leg:
+        passes.update(PMC_L2_PASS)  # the fleet's shared model is read from L2: its hit rate
+    for name, counters in passes.items():
         t0 = time.time()
         cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", os.path.join(out, "run", name), "-o", "run",
                "--", *child]

@@ -175,6 +175,10 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    8 steps), and completes before any call that reads the records: export,
                                    save, learning on, htm_status / htm_counters, htm_flush.  Results and
                                    state are those of the undeferred step.  0: count every phase 2 in full */
+#define HTM_OPT_FLUSH_MODE 11   /* where the deferred-write flush runs: 0 on the engine's own HIP stream
+                                   beside the next steps, 1 on the step stream after them (full width).
+                                   Results are identical; the default is chosen by measurement from the
+                                   engine size (deferred dutyCycle() writes) */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued
@@ -419,6 +423,10 @@ int htm_cls_import_state(htm_classifier* cls, int32_t region, int32_t stream_beg
 
 const char* htm_last_error(void);
 int32_t htm_abi_version(void);
+/* How the library was built: "<unit> <optimisation level>;..." for every
+ * translation unit (LLVM's gfx950 verifier has rejected some units at -O3;
+ * those build at -O2 or -O1, csrc/cc.sh), then the compiler and the target. */
+const char* htm_build_info(void);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,7 @@ OPT_FUSED = 5
 OPT_RUN_CHUNK = 6
 OPT_RUN_UNIT = 7
 OPT_DEFER_DUTY = 10
+OPT_FLUSH_MODE = 11
 
 
 class HtmConfig(ctypes.Structure):
@@ -111,7 +112,7 @@ EXPORTED = [
     "htm_step", "htm_run", "htm_step_sdr", "htm_run_sdr", "htm_get_output", "htm_output_bytes", "htm_state_bytes", "htm_export_state",
     "htm_import_state", "htm_reset_tm", "htm_save", "htm_load", "htm_replicate_stream", "htm_n_streams",
     "htm_get_config", "htm_device_bytes", "htm_sp_perm_rows_used", "htm_frozen_index_valid", "htm_last_error", "htm_abi_version",
-    "htm_profile_read", "htm_counters", "htm_debug_stamps",
+    "htm_profile_read", "htm_counters", "htm_debug_stamps", "htm_build_info",
     "htm_slo_create", "htm_slo_destroy", "htm_slo_record", "htm_slo_stats", "htm_create_fleet", "htm_is_fleet", "htm_flush",
     "htm_likelihood_create", "htm_likelihood_destroy", "htm_likelihood_step",
     "htm_cls_create", "htm_cls_destroy", "htm_cls_compute", "htm_cls_status", "htm_cls_state_bytes",
@@ -182,6 +183,7 @@ def lib():
     L.htm_frozen_index_valid.restype = i32
     L.htm_last_error.restype = ctypes.c_char_p
     L.htm_abi_version.restype = i32
+    L.htm_build_info.restype = ctypes.c_char_p
     L.htm_profile_read.argtypes = [vp, P(ctypes.c_double)]
     L.htm_counters.argtypes = [vp, P(ctypes.c_uint64)]
     L.htm_debug_stamps.argtypes = [vp, P(ctypes.c_uint64)]
@@ -206,6 +208,25 @@ def lib():
     L.htm_slo_stats.argtypes = [vp, P(ctypes.c_int64), vp]
     _lib = L
     return L
+
+
+def build_info() -> dict:
+    """{translation unit: optimisation level} of the loaded library, plus
+    "compiler" / "arch" (htm_build_info; csrc/cc.sh records the levels)."""
+    raw = lib().htm_build_info().decode()
+    out = {}
+    for part in raw.split(";"):
+        part = part.strip()
+        if not part:
+            continue
+        if part.startswith("HIP version") or part.startswith("hipcc"):
+            out["compiler"] = part
+        elif part.startswith("arch "):
+            out["arch"] = part[5:]
+        else:
+            unit, _, lvl = part.rpartition(" ")
+            out[unit] = lvl
+    return out
 
 
 def check(code: int):

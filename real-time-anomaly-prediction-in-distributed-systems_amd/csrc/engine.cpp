@@ -633,6 +633,11 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         }
         e->defer = value ? 1 : 0;
     }
+    else if (opt == HTM_OPT_FLUSH_MODE) {
+        if (value != 0 && value != 1) return htm_fail(HTM_E_INVALID, "flush mode must be 0 (beside the steps) or 1 (on the step stream)");
+        if (int r = flush_sync(e)) return r;
+        e->flush_mode = value;
+    }
     else if (opt == HTM_OPT_RUN_UNIT) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
         e->run_unit = value;
@@ -672,6 +677,7 @@ static int alloc_dlog(htm_engine* e) {
     ALLOC(e->tm.fx_dn, uint32_t, S);
     ALLOC(e->tm.fx_dflushed, uint32_t, S);
     ALLOC(e->tm.fx_dsnap, uint32_t, S);
+    ALLOC(e->tm.fx_dupto, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
     ALLOC(e->tm.fx_fwork, uint32_t, 4);
     ALLOC(e->tm.fx_fjobs, uint32_t, S * (size_t)d.fx_dcap);
@@ -753,6 +759,7 @@ static int build_fx(htm_engine* e, hipStream_t st) {
         HIP_TRY(hipMemsetAsync(e->tm.fx_dn, 0, (size_t)e->n * 4, st));
         HIP_TRY(hipMemsetAsync(e->tm.fx_dflushed, 0, (size_t)e->n * 4, st));
         HIP_TRY(hipMemsetAsync(e->tm.fx_dsnap, 0, (size_t)e->n * 4, st));
+        HIP_TRY(hipMemsetAsync(e->tm.fx_dupto, 0, (size_t)e->n * 4, st));
     }
     if (launch_tm_fx_rank(d, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "fx rank launch");
     if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return htm_fail(HTM_E_HIP, "fx count launch");

@@ -198,11 +198,21 @@ struct TmBufs {
     uint32_t* fx_dhash;            // [S][fx_dcap] hash of the set
     uint32_t* fx_dn;               // [S] entries logged (monotonic)
     uint32_t* fx_dflushed;         // [S] entries flushed
-    uint32_t* fx_dsnap;            // [S] fx_dn when the running flush was enqueued (its upper bound)
+    uint32_t* fx_dsnap;            // [S] fx_dn when the latest flush was enqueued (step stream)
+    uint32_t* fx_dupto;            // [S] the bound the running flush's job builder took from fx_dsnap:
+                                   //     the flush replays [fx_dflushed, fx_dupto) and its done kernel
+                                   //     advances fx_dflushed to exactly that (never to a later snapshot)
     uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
-    uint32_t* fx_fwork;            // [4] flush job counter, error flags (16: qualifying-list overflow), jobs
+    uint32_t* fx_fwork;            // [4] flush job counter, error flags (FX_ERR_*), jobs
     uint32_t* fx_fjobs;            // [S * fx_dcap] the running flush's entries (stream * fx_dcap + ring slot)
 };
+
+// deferred-log flush error flags (fx_fwork[1]; htm_status / htm_counters)
+#define FX_ERR_QCAP 16u   // a replayed phase 2 overflowed q_cap (as in the step: results invalid)
+#define FX_ERR_RING 64u   // fx_dupto - fx_dflushed > fx_dcap: ring counters inconsistent (entries skipped)
+#define FX_ERR_JOBS 128u  // the job list would pass S * fx_dcap entries (entries skipped)
+#define FX_ERR_JOB 256u   // a job names a stream >= n, a slot >= fx_dcap or a set longer than
+                          // max_act_cells (job skipped)
 
 #define FX_FLUSH_WG 1024  // persistent workgroups of tm_fx_flush_kernel (each has its own scratch list)
 

@@ -342,23 +342,37 @@ int tm_configure_lds(const DevCfg& c) {
 // its own work).  tm_fx_flush_done_kernel then marks the entries flushed and
 // clears fx_fwork[0] (zero at allocation) for the next flush.
 // The flush runs on its own stream beside later steps: it replays the entries
-// [fx_dflushed, fx_dsnap) -- fx_dsnap is the snapshot of fx_dn taken on the
-// step stream when the flush was enqueued -- and the steps only append to ring
-// slots outside that range (a step reads fx_dflushed, which moves only when
-// a flush is complete; a stale read leaves it fewer free slots, never more).
+// [fx_dflushed, fx_dupto) -- fx_dupto is the value of fx_dsnap (the snapshot
+// of fx_dn taken on the step stream when a flush was enqueued) its job
+// builder read -- and the steps only append to ring slots outside that range
+// (a step reads fx_dflushed, which moves only when a flush is complete, and
+// only to that flush's fx_dupto; a stale read leaves it fewer free slots,
+// never more).  Every job is checked before use (FX_ERR_JOB): a bad one is
+// skipped and flagged, never dereferenced.
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
-    const uint32_t total = b.fx_fwork[2];  // the job list (tm_fx_jobs_kernel, the launch before)
+    const uint32_t dcap = (uint32_t)c.fx_dcap;
+    uint32_t total = b.fx_fwork[2];  // the job list (tm_fx_jobs_kernel, the launch before)
+    if (total > (uint32_t)n * dcap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
+        total = (uint32_t)n * dcap;
+    }
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) job = atomicAdd(&b.fx_fwork[0], 1u);
         __syncthreads();
         const uint32_t jj = __builtin_amdgcn_readfirstlane(job);
         if (jj >= total) break;
-        const uint32_t j = b.fx_fjobs[jj];  // stream * dcap + ring slot
-        const int s = (int)(j / (uint32_t)c.fx_dcap);
-        const uint32_t i = j % (uint32_t)c.fx_dcap;
+        const uint32_t j = __builtin_amdgcn_readfirstlane(b.fx_fjobs[jj]);  // stream * dcap + ring slot
+        const uint32_t su = j / dcap;
+        const uint32_t i = j % dcap;
+        const uint32_t len0 = su < (uint32_t)n ? (uint32_t)b.fx_dlen[(size_t)su * dcap + i] : 0xFFFFFFFFu;
+        if (su >= (uint32_t)n || len0 > (uint32_t)c.max_act_cells) {
+            if (threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOB);
+            continue;
+        }
+        const int s = (int)su;
         Tm t;
         tm_bind<false, true>(t, c, b, s, s, lds);
         t.q1 = b.fx_fq + (size_t)blockIdx.x * c.q_cap;
@@ -372,15 +386,17 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         }
         wg_clear(t.infA, c.cw);
         __syncthreads();
-        const size_t ei = (size_t)s * c.fx_dcap + i;
-        const uint32_t len = b.fx_dlen[ei];
+        const size_t ei = (size_t)s * dcap + i;
         const uint16_t* cl = b.fx_dlog + ei * fx_dstride(c);
-        for (uint32_t k = threadIdx.x; k < len; k += TM_NT) atomicOr(&t.infA[cl[k] >> 5], 1u << (cl[k] & 31));
+        for (uint32_t k = threadIdx.x; k < len0; k += TM_NT) {
+            const uint32_t cell = cl[k];
+            if (cell < (uint32_t)c.ncells) atomicOr(&t.infA[cell >> 5], 1u << (cell & 31));
+        }
         __syncthreads();
         collect_frozen(t, c.act_thr, FX_WIN);
         __syncthreads();
         if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)c.q_cap) {
-            atomicOr(&b.fx_fwork[1], 16u);  // qualifying-list overflow, as in the step (htm_status)
+            atomicOr(&b.fx_fwork[1], FX_ERR_QCAP);  // qualifying-list overflow, as in the step (htm_status)
             sh->qn = c.q_cap;
         }
         __syncthreads();
@@ -394,18 +410,30 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
 // hash and length first, then the cells themselves) is dropped: the flush of
 // the earlier one makes the same one-time record writes.  Steps append to the
 // ring beside this kernel but never into [fx_dflushed, fx_dsnap), so the
-// batch is stable.  One workgroup per stream.
+// batch is stable.  The bound taken is stored in fx_dupto: a later snapshot
+// the step stream takes while this flush runs (flushes every few steps, a
+// flush slower than that) moves fx_dsnap, not what this flush completes --
+// its done kernel advances fx_dflushed to fx_dupto, so no entry is marked
+// flushed without having been replayed.  One workgroup per stream.
 __global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n) {
     __shared__ uint32_t hsh[64], len[64], keep[64];
     const int s = blockIdx.x;
-    const uint32_t f = b.fx_dflushed[s], p = b.fx_dsnap[s] - f;  // p <= fx_dcap <= 64
-    if (p == 0 || p > 64) return;
     const uint32_t dcap = (uint32_t)c.fx_dcap;
+    const uint32_t f = b.fx_dflushed[s], u = b.fx_dsnap[s], p = u - f;
+    // the ring invariant: fx_dflushed <= fx_dsnap <= fx_dflushed + fx_dcap
+    // (a step appends only while fewer than fx_dcap entries are unflushed)
+    const bool bad = p > dcap || dcap > 64u;
+    if (threadIdx.x == 0) {
+        b.fx_dupto[s] = bad ? f : u;
+        if (bad) atomicOr(&b.fx_fwork[1], FX_ERR_RING);
+    }
+    if (p == 0 || bad) return;
     const size_t mac = fx_dstride(c);
     auto entry = [&](uint32_t i) { return (size_t)s * dcap + (f + i) % dcap; };
     if (threadIdx.x < p) {
         hsh[threadIdx.x] = 0u;
-        len[threadIdx.x] = b.fx_dlen[entry(threadIdx.x)];
+        const uint32_t l = b.fx_dlen[entry(threadIdx.x)];
+        len[threadIdx.x] = l < (uint32_t)mac ? l : (uint32_t)mac;  // (a longer one is flagged by the flush)
     }
     __syncthreads();
     for (uint32_t i = 0; i < p; i++) {
@@ -450,15 +478,20 @@ __global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int
         uint32_t m = 0;
         for (uint32_t i = 0; i < p; i++) m += keep[i];
         uint32_t base = atomicAdd(&b.fx_fwork[2], m);
-        for (uint32_t i = 0; i < p; i++)
-            if (keep[i]) b.fx_fjobs[base++] = (uint32_t)s * dcap + (f + i) % dcap;
+        const uint32_t cap = (uint32_t)n * dcap;
+        for (uint32_t i = 0; i < p; i++) {
+            if (!keep[i]) continue;
+            if (base < cap) b.fx_fjobs[base] = (uint32_t)s * dcap + (f + i) % dcap;
+            else atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
+            base++;
+        }
     }
 }
 
-// after a flush: every snapshot entry is flushed; the counters restart
+// after a flush: the entries its job builder took are flushed; the counters restart
 __global__ void tm_fx_flush_done_kernel(TmBufs b, int n) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < n) b.fx_dflushed[s] = b.fx_dsnap[s];
+    if (s < n) b.fx_dflushed[s] = b.fx_dupto[s];
     if (s == 0) {
         b.fx_fwork[0] = 0u;
         b.fx_fwork[2] = 0u;

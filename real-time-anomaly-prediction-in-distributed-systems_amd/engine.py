@@ -236,6 +236,11 @@ class HTMEngine:
     def defer_duty(self, on: bool):
         check(self._L.htm_set_option(self.h, _lib.OPT_DEFER_DUTY, int(on)))
 
+    def flush_mode(self, mode: int):
+        """Where the deferred-write flush runs: 0 beside the next steps on the
+        engine's own HIP stream, 1 on the step stream (results identical)."""
+        check(self._L.htm_set_option(self.h, _lib.OPT_FLUSH_MODE, int(mode)))
+
     def sp_perm_rows_used(self) -> int:
         """Paged SP permanences: pool rows handed out (0 for a dense engine)."""
         return int(self._L.htm_sp_perm_rows_used(self.h))

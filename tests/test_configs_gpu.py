@@ -79,6 +79,46 @@ def test_config4_fleet_131072_streams_vs_oracle(rt, fleet_model, traces):
     assert 0 < np.count_nonzero(got == 0) < got.size
 
 
+def test_config4_fleet_flush_beside_the_steps(rt, fleet_model, traces):
+    """The deferred-write flush beside the steps (HTM_OPT_FLUSH_MODE 0) at fleet
+    scale: 131,072 streams, 8-entry logs, a flush enqueued every 4 steps, each
+    flush slower than those 4 steps -- so snapshots are taken while earlier
+    flushes still run (the round-3 overlap).  96 lockstep steps: 8 sampled
+    streams equal oracle clones at every step, the flush reports no error flag
+    (ring / job-list / job checks, tm.hip), and the shared model's segment
+    records (dutyCycle cache included) equal those of the same fleet flushed on
+    the step stream -- no deferred write is lost."""
+    model, orc = fleet_model
+    n, T = 131072, 96
+    vals = fleet_inputs(traces, n, T, seed=31)
+    v = torch.tensor(vals, device="cuda")
+    out = {}
+    for mode in (0, 1):
+        fl = rt.HTMEngine.fleet(model, n, q_capacity=4096)
+        fl.flush_mode(mode)
+        scores = torch.empty((T, n), dtype=torch.float32, device="cuda")
+        for k in range(T):
+            fl.step(v[k], out=scores[k])
+        fl.flush()
+        torch.cuda.synchronize()
+        c = fl.counters()
+        assert c["error"] == 0, f"mode {mode}: error flags {c['error']:#x}"
+        fl.status()
+        out[mode] = (scores.cpu().numpy(), fl.export_state("tm_seg_duty", 0, 1), fl.export_state("tm_seg_meta", 0, 1),
+                     c)
+        fl.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1]), "segment dutyCycle records differ: deferred writes lost"
+    assert np.array_equal(out[0][2], out[1][2])
+    for key in ("inf_phase2", "inf_backtracks"):
+        assert out[0][3][key] == out[1][3][key], key
+    got = out[0][0]
+    for s in [0, 5, 4097, 33333, 65536 + 777, n - 1]:
+        o = orc.clone()
+        want = np.array([o.step([vals[k, s]], False, False) for k in range(T)], np.float32)
+        assert np.array_equal(got[:, s], want), f"stream {s}"
+
+
 def test_config3_many_fresh_streams_learning(rt, oracle_mod):
     """512 fresh streams (seed per stream) with SP+TM learning on: 8 sampled
     streams match independent oracle models at every step; two of them match

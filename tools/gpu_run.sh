@@ -14,5 +14,5 @@ for spec in "$@"; do
     rc=$?
     echo "$name rc=$rc $(( $(date +%s) - t0 ))s"
     tail -3 "$OUT/$name.log"
-    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc $rc)"; exit $rc; fi
+    if [ $rc -ne 0 ] && { [ $rc -ne 1 ] || [ "${STRICT:-0}" = 1 ]; }; then echo "stopping after $name (rc $rc)"; exit $rc; fi
 done

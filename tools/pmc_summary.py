@@ -7,6 +7,7 @@ command (tools/gpu_prof.sh):
   pmc_rd/     TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
   pmc_fetch/  FETCH_SIZE
   pmc_wr/     WRITE_SIZE TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
+  pmc_l2/     TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum (optional: fleets, whose shared model is L2-served)
   prof/       --kernel-trace --stats (kernel_stats.csv is copied along)
 Counters are per dispatch; the median over the dispatches of each kernel is
 reported.  Read bytes are counted from the L2 memory-side read requests by
@@ -47,10 +48,14 @@ def med(d, k, c):
 
 
 def summarise(run):
-    rd, fe, wr = (load_pass(os.path.join(run, p)) for p in ("pmc_rd", "pmc_fetch", "pmc_wr"))
+    rd, fe, wr, l2 = (load_pass(os.path.join(run, p)) for p in ("pmc_rd", "pmc_fetch", "pmc_wr", "pmc_l2"))
     kernels = {}
-    for k in set(rd) | set(fe) | set(wr):
+    for k in set(rd) | set(fe) | set(wr) | set(l2):
         e = {}
+        hit, miss, req = (med(l2, k, c) for c in ("TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum"))
+        if None not in (hit, miss):
+            e["l2"] = {"hit": hit, "miss": miss, "req": req,
+                       "hit_rate": round(hit / (hit + miss), 4) if hit + miss > 0 else None}
         r32, r64, r128, rall = (med(rd, k, c) for c in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
                                                        "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_sum"))
         w64, wall = med(wr, k, "TCC_EA0_WRREQ_64B_sum"), med(wr, k, "TCC_EA0_WRREQ_sum")
