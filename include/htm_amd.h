@@ -199,10 +199,10 @@ int htm_counters(htm_engine* eng, uint64_t* out8);
 
 /* Diagnostic builds only (libhtm_amd_stamps.so, -DHTM_STAMPS): per-phase
  * shader-cycle stamps of the TM kernel summed over streams since the last
- * call (out96[0..23]) and event counts (out96[24..47]), then the same over
+ * call (out128[0..31]) and event counts (out128[32..63]), then the same over
  * the tail steps only -- stream-steps whose TM part took >= 2^18 cycles
- * (out96[48..95]); HTM_E_STATE in the product library. */
-int htm_debug_stamps(htm_engine* eng, uint64_t* out96);
+ * (out128[64..127]); HTM_E_STATE in the product library. */
+int htm_debug_stamps(htm_engine* eng, uint64_t* out128);
 
 /* Synchronise and check every stream's overflow flags (HTM_E_CAPACITY). */
 int htm_status(htm_engine* eng);
@@ -314,7 +314,11 @@ typedef struct {
 /* TM reset (BacktrackingTM.reset) of every stream. */
 int htm_reset_tm(htm_engine* eng, void* stream);
 
-/* Save / load the whole engine (config + every region) to one file. */
+/* Save / load the whole engine (config + every region) to one file.  The
+ * deferred dutyCycle() writes are completed first.  A fleet (htm_create_fleet)
+ * saves its shared model once and every stream's own state, and loads back as
+ * a fleet: a run saved mid-way continues bit-exactly from the loaded file
+ * (NetworkModel.py:123-125 saves before the step, ModelTesting.py:176 reloads). */
 int htm_save(htm_engine* eng, const char* path);
 int htm_load(const char* path, int32_t device, htm_engine** out);
 

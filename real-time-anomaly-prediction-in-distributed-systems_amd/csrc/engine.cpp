@@ -425,6 +425,7 @@ static int allocate(htm_engine* e) {
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
     ALLOC(e->tm.dbg, uint64_t, S * 4 * HTM_NSTAMP);
+    ALLOC(e->sp.dbg, uint64_t, S * 2);
 #endif
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
@@ -1002,17 +1003,26 @@ int htm_counters(htm_engine* e, uint64_t* out8) {
     return HTM_OK;
 }
 
-int htm_debug_stamps(htm_engine* e, uint64_t* out96) {
-    if (!e || !out96) return htm_fail(HTM_E_INVALID, "bad arguments");
+// count slots of the SP paged-row replays (tm_core.h SC_REPLAY, SC_REPLAYCYC)
+#define SC_REPLAY_IDX 18
+
+int htm_debug_stamps(htm_engine* e, uint64_t* out128) {
+    if (!e || !out128) return htm_fail(HTM_E_INVALID, "bad arguments");
     if (!e->tm.dbg) return htm_fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
     HIP_TRY(hipDeviceSynchronize());
     const int W = 4 * HTM_NSTAMP;
-    std::vector<uint64_t> h((size_t)e->n * W);
+    std::vector<uint64_t> h((size_t)e->n * W), r((size_t)e->n * 2);
     HIP_TRY(hipMemcpy(h.data(), e->tm.dbg, h.size() * 8, hipMemcpyDeviceToHost));
-    for (int k = 0; k < W; k++) out96[k] = 0;
-    for (int s = 0; s < e->n; s++)
-        for (int k = 0; k < W; k++) out96[k] += h[(size_t)s * W + k];
+    HIP_TRY(hipMemcpy(r.data(), e->sp.dbg, r.size() * 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < W; k++) out128[k] = 0;
+    for (int s = 0; s < e->n; s++) {
+        for (int k = 0; k < W; k++) out128[k] += h[(size_t)s * W + k];
+        // SP paged-row replays (not attributable to tail steps)
+        out128[HTM_NSTAMP + SC_REPLAY_IDX] += r[(size_t)s * 2];
+        out128[HTM_NSTAMP + SC_REPLAY_IDX + 1] += r[(size_t)s * 2 + 1];
+    }
     HIP_TRY(hipMemset(e->tm.dbg, 0, h.size() * 8));
+    HIP_TRY(hipMemset(e->sp.dbg, 0, r.size() * 8));
     return HTM_OK;
 }
 
@@ -1487,26 +1497,31 @@ int htm_status(htm_engine* e) {
 // ---------------------------------------------------------------------------
 // save / load: "HTMAMD01", abi, config, n, learning flags, then regions --
 // the SP checkpoints first, so a paged engine's permanences are imported
-// against the initial values they were exported with
+// against the initial values they were exported with.  A fleet's file starts
+// "HTMFLT01" and carries its q_capacity after the flags; its model regions
+// (SP permanences / connections, the TM segment pool) are stored once, its
+// per-stream regions (TM state, RDSE maps, SP counters) for every stream.
 static int save_order(int k) { return k == 0 ? HTM_ST_SP_PERM_CKPT : k < HTM_ST_SP_PERM_CKPT ? k : k + 1; }
 
 int htm_save(htm_engine* e, const char* path) {
     if (!e || !path) return htm_fail(HTM_E_INVALID, "bad arguments");
-    if (e->fleet) return htm_fail(HTM_E_STATE, "fleet engines are not saved: save the model engine they were built from");
+    if (int rf = flush_sync(e)) return rf;  // the deferred dutyCycle() writes are part of the state
     FILE* f = std::fopen(path, "wb");
     if (!f) return htm_fail(HTM_E_IO, "cannot open %s", path);
-    const char magic[8] = {'H', 'T', 'M', 'A', 'M', 'D', '0', '1'};
+    const char magic[8] = {'H', 'T', 'M', e->fleet ? 'F' : 'A', e->fleet ? 'L' : 'M', e->fleet ? 'T' : 'D', '0', '1'};
     int32_t abi = HTM_ABI_VERSION;
     bool ok = std::fwrite(magic, 8, 1, f) == 1 && std::fwrite(&abi, 4, 1, f) == 1 &&
               std::fwrite(&e->cfg, sizeof(htm_config), 1, f) == 1 && std::fwrite(&e->n, 4, 1, f) == 1 &&
               std::fwrite(&e->sp_learn, 4, 1, f) == 1 && std::fwrite(&e->tm_learn, 4, 1, f) == 1;
+    if (ok && e->fleet) ok = std::fwrite(&e->dc.q_cap, 4, 1, f) == 1;
     std::vector<uint8_t> buf;
     for (int k = 0; ok && k < HTM_ST_COUNT; k++) {
         const int id = save_order(k);
         const Region& r = e->regions[id];
-        uint64_t nb = (uint64_t)r.per_stream * e->n;
+        const int32_t cnt = region_count(e, id);
+        uint64_t nb = (uint64_t)r.per_stream * cnt;
         buf.resize(nb);
-        if (htm_export_state(e, id, 0, e->n, buf.data(), nb)) { ok = false; break; }
+        if (htm_export_state(e, id, 0, cnt, buf.data(), nb)) { ok = false; break; }
         int32_t rid = id;
         ok = std::fwrite(&rid, 4, 1, f) == 1 && std::fwrite(&nb, 8, 1, f) == 1 && std::fwrite(buf.data(), 1, nb, f) == nb;
     }
@@ -1521,18 +1536,21 @@ int htm_load(const char* path, int32_t device, htm_engine** out) {
     FILE* f = std::fopen(path, "rb");
     if (!f) return htm_fail(HTM_E_IO, "cannot open %s", path);
     char magic[8];
-    int32_t abi = 0, n = 0, spl = 1, tml = 1;
+    int32_t abi = 0, n = 0, spl = 1, tml = 1, qcap = 0;
     htm_config cfg;
-    bool ok = std::fread(magic, 8, 1, f) == 1 && std::memcmp(magic, "HTMAMD01", 8) == 0 &&
+    bool ok = std::fread(magic, 8, 1, f) == 1 &&
+              (std::memcmp(magic, "HTMAMD01", 8) == 0 || std::memcmp(magic, "HTMFLT01", 8) == 0) &&
               std::fread(&abi, 4, 1, f) == 1 && abi == HTM_ABI_VERSION &&
               std::fread(&cfg, sizeof(cfg), 1, f) == 1 && std::fread(&n, 4, 1, f) == 1 &&
               std::fread(&spl, 4, 1, f) == 1 && std::fread(&tml, 4, 1, f) == 1;
+    const bool fleet = ok && magic[3] == 'F';
+    if (ok && fleet) ok = std::fread(&qcap, 4, 1, f) == 1 && qcap >= 64;
     if (!ok) {
         std::fclose(f);
         return htm_fail(HTM_E_IO, "%s is not an engine file of ABI %d", path, HTM_ABI_VERSION);
     }
     htm_engine* e = nullptr;
-    int r = create_uninit(&cfg, n, device, &e);
+    int r = create_uninit(&cfg, n, device, &e, fleet ? qcap : 0);
     if (r) {
         std::fclose(f);
         return r;
@@ -1540,22 +1558,23 @@ int htm_load(const char* path, int32_t device, htm_engine** out) {
     std::vector<uint8_t> buf;
     for (int i = 0; ok && i < HTM_ST_COUNT; i++) {
         const int k = save_order(i);
+        const int32_t cnt = region_count(e, k);
         int32_t rid;
         uint64_t nb;
         ok = std::fread(&rid, 4, 1, f) == 1 && std::fread(&nb, 8, 1, f) == 1 && rid == k &&
-             nb == (uint64_t)e->regions[k].per_stream * n;
+             nb == (uint64_t)e->regions[k].per_stream * cnt;
         if (!ok) break;
         buf.resize(nb);
         ok = std::fread(buf.data(), 1, nb, f) == nb;
-        if (ok && import_region(e, k, 0, n, buf.data(), nb, false)) ok = false;
+        if (ok && import_region(e, k, 0, cnt, buf.data(), nb, false)) ok = false;
     }
     std::fclose(f);
     if (!ok) {
         htm_destroy(e);
         return htm_fail(HTM_E_IO, "truncated or inconsistent engine file %s", path);
     }
-    e->sp_learn = spl;
-    e->tm_learn = tml;
+    e->sp_learn = fleet ? 0 : spl;
+    e->tm_learn = fleet ? 0 : tml;
     *out = e;
     return HTM_OK;
 }

@@ -138,6 +138,7 @@ struct SpBufs {
     uint16_t* enc_in;
     int32_t* enc_bucket;  // [S][4]
     uint64_t* rdse_seeds; // [S] RDSE seed per stream
+    uint64_t* dbg;        // [S][2] paged-row replays and their lane-0 cycles (HTM_STAMPS builds only, else null)
 };
 
 struct TmBufs {
@@ -221,7 +222,7 @@ struct TmBufs {
 // Diagnostic phase stamps (HTM_STAMPS builds only): thread 0 charges the
 // shader cycles since its previous stamp to bucket k.  Compiled out of the
 // product library.
-#define HTM_NSTAMP 24  // stamp buckets; the debug record per stream is 2 x HTM_NSTAMP words
+#define HTM_NSTAMP 32  // stamp buckets; the debug record per stream is 4 x HTM_NSTAMP words
 #ifdef HTM_STAMPS
 #define STAMP(t, k)                                                     \
     do {                                                                \

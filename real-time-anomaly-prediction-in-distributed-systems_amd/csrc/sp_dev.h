@@ -42,6 +42,9 @@ struct SpShared {
     int32_t nbump;
     uint16_t bump[HTM_MAXNW * 32 > 4096 ? 4096 : HTM_MAXNW * 32];
     float red[16];  // per-wave maxima (<= 16 waves)
+#ifdef HTM_STAMPS
+    uint64_t st_t_learn;  // shader clock when the learning part began (0: no learning)
+#endif
     template <class F>
     __device__ __forceinline__ void each_active_input(const DevCfg&, F&& f) const {
         for (int a = 0; a < n_act_inputs; a++) f(act_inputs[a]);
@@ -471,10 +474,75 @@ __device__ __forceinline__ void sp_replay_init(const SpInitCfg& c, int s, int co
     }
 }
 
-// The initial permanences of one column into a fresh pool row: out of line,
-// so the rare replay does not weigh on the fused kernels' register budget
+// The initial permanences of column col of stream s into a fresh pool row,
+// replayed by the whole wave -- sp_replay_init's draws in the same order,
+// without its per-draw lane-0 bookkeeping: the generator runs wave-uniformly
+// (its 31 words are the same in every lane, in scalar registers), lane
+// k % 64 keeps the four draws of permanence rank k, and each 64 ranks are
+// computed and stored by the 64 lanes at once (coalesced).  Out of line, so
+// the replay does not weigh on the fused kernels' register budget.  Call with
+// every lane of the wave.
 static __device__ __attribute__((noinline)) void sp_regen_row(SpInitCfg c, int s, int col, float* row) {
-    sp_replay_init(c, s, col, col, [&](int, int k, float p) { row[k] = p; });
+    const uint32_t l = (uint32_t)lane_id();
+    const int pw = c.nin_pad >> 5;
+    const int g0 = col - col % SP_CKPT_COLS;
+    const uint32_t* pot = c.potmask + (size_t)s * c.ncol * pw;
+    const uint32_t npot = (uint32_t)c.n_potential;
+    const uint32_t npd = 4u * npot;
+    // sampling draws of the group's columns g0..col, one lane each
+    uint32_t myd = 0;
+    if (l < (uint32_t)SP_CKPT_COLS && g0 + (int)l <= col) myd = sp_sample_draws(c, pot + (size_t)(g0 + (int)l) * pw, g0 + (int)l);
+    uint32_t sk = 0;  // draws to discard before the column's first permanence draw (< 2^31)
+    for (int k = 0; k < col - g0; k++) sk += (uint32_t)__builtin_amdgcn_readlane((int)myd, k) + npd;
+    sk += (uint32_t)__builtin_amdgcn_readlane((int)myd, col - g0);
+    const uint32_t* ck = c.ckpt + ((size_t)s * c.n_ckpt + (size_t)(g0 / SP_CKPT_COLS)) * SP_CKPT_WORDS;
+    uint32_t i = 0;                    // the column's draws taken so far
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;  // this lane's draws of its current rank
+    // one draw: discarded, or the next of the column (true when the column is complete)
+    auto take = [&](uint32_t raw) -> bool {
+        if (sk) {
+            sk--;
+            return false;
+        }
+        const uint32_t k = i >> 2, ph = i & 3u;
+        const bool mine = (k & 63u) == l;
+        if (ph == 0u) q0 = mine ? raw : q0;
+        else if (ph == 1u) q1 = mine ? raw : q1;
+        else if (ph == 2u) q2 = mine ? raw : q2;
+        else {
+            q3 = mine ? raw : q3;
+            // a round of 64 ranks complete (or the column's last): every lane
+            // computes its rank's permanence, one coalesced store
+            if ((k & 63u) == 63u || k + 1u == npot) {
+                if (l <= (k & 63u)) {
+                    bool isconn;
+                    row[(k & ~63u) + l] = sp_init_value(c, q0, q1, q2, q3, isconn);
+                }
+            }
+        }
+        return ++i == npd;
+    };
+    // draws the checkpoint's block had generated but not handed out yet
+    bool done = false;
+    const uint32_t pend = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[31]);
+    for (uint32_t j = pend; j < 31u && !done; j++) done = take((uint32_t)__builtin_amdgcn_readfirstlane((int)ck[32 + j]));
+    uint32_t st[31];
+#pragma unroll
+    for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[j]);
+    while (!done) {
+        if (sk >= 31u) {
+#pragma unroll
+            for (int j = 0; j < 31; j++) st[(3 + j) % 31] += st[j];
+            sk -= 31u;
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < 31; j++) {
+            const int f = (3 + j) % 31;
+            st[f] += st[j];
+            if (!done) done = take((st[f] >> 1) & 0x7fffffffu);
+        }
+    }
 }
 
 // Permanence row of column col of stream s (wave-uniform; every lane of the
@@ -486,15 +554,13 @@ __device__ __forceinline__ float* sp_perm_row(const DevCfg& c, const SpBufs& b, 
     const size_t ms = (size_t)model_stream(c, s);
     if (!PAGED_OK || !c.sp_paged) return b.perm + (ms * c.ncol + col) * c.n_potential;
     uint32_t r = 0, fresh = 0;
+    uint32_t* slot = b.prow + ms * c.ncol + col;
     if (lane_id() == 0) {
-        uint32_t* slot = b.prow + ms * c.ncol + col;
         r = *slot;
         if (r == SP_ROW_NONE) {
             const unsigned long long x = atomicAdd(b.pool_next, 1ull);
             if (x < c.pool_rows) {
                 r = (uint32_t)x;
-                sp_regen_row(sp_init_cfg(c, b), (int)ms, col, b.pool + (size_t)r * c.pool_stride);
-                *slot = r;
                 fresh = 1;
             } else {
                 atomicOr(&b.err[s], SP_ERR_POOL);
@@ -502,9 +568,25 @@ __device__ __forceinline__ float* sp_perm_row(const DevCfg& c, const SpBufs& b, 
         }
     }
     r = (uint32_t)__shfl((int)r, 0, 64);
-    // lane 0's stores of a fresh row before the wave's loads of it (rows are
-    // 128-byte aligned and handed out once, so no cache line holds an older copy)
-    if (__shfl((int)fresh, 0, 64)) __threadfence();
+    if (__shfl((int)fresh, 0, 64)) {
+        // the wave writes the initial values into the fresh row, then lane 0
+        // publishes it; the wave's stores land before its loads of the row
+        // (rows are 128-byte aligned and handed out once, so no cache line
+        // holds an older copy)
+#ifdef HTM_STAMPS
+        const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+#endif
+        sp_regen_row(sp_init_cfg(c, b), (int)ms, col, b.pool + (size_t)r * c.pool_stride);
+#ifdef HTM_STAMPS
+        if (b.dbg && lane_id() == 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 2]), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 2 + 1]),
+                      (unsigned long long)(__builtin_amdgcn_s_memtime() - t0_));
+        }
+#endif
+        if (lane_id() == 0) *slot = r;
+        __threadfence();
+    }
     if (r == SP_ROW_NONE) return nullptr;
     return b.pool + (size_t)r * c.pool_stride;
 }
@@ -656,6 +738,11 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     const int nact = sh.nact < HTM_MAXACT ? sh.nact : HTM_MAXACT;
     if (t < nact) b.act[(size_t)s * HTM_MAXACT + t] = sh.actlist[t];
     if (t == 0) b.nact[s] = (uint32_t)nact;
+#ifdef HTM_STAMPS
+    if constexpr (std::is_same<SH, SpShared>::value) {
+        if (t == 0) sh.st_t_learn = LEARN ? __builtin_amdgcn_s_memtime() : 0ull;
+    }
+#endif
     if (!LEARN) return;  // (callers synchronise before reading b.act)
     // ---- adaptSynapses_: one wave per active column
     for (int a = wave_id(); a < nact; a += blockDim.x >> 6) sp_adapt_column<PAGED_OK>(c, b, s, sh.actlist[a], sh.in, 0);

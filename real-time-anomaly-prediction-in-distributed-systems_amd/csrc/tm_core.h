@@ -106,12 +106,21 @@ struct Tm {
 // stamp buckets (HTM_STAMPS): where one stream-step's cycles go
 enum {
     SB_LOAD = 0, SB_P1, SB_LIST, SB_WINPRE, SB_STREAM, SB_QSCAN, SB_FIN1, SB_FIN2, SB_BT, SB_LEARN, SB_WB,
-    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER, SB_SP, SB_NORM
+    SB_SCAN, SB_SORT, SB_SUMS, SB_OWNER, SB_SLOAD, SB_COUNT, SB_FCLR, SB_CPC, SB_DEFER, SB_SP, SB_NORM,
+    // learning (round 4): learn-phase pool scans (scan_best), queued segment
+    // updates, wave 0's serial adapt / create / update-building, the learn
+    // backtrack's state copies, pool compaction, the SP's learning part
+    // (adaptSynapses_ incl. paged-row replays, duty cycles, weak-column bumps)
+    SB_LSCAN, SB_LUPD, SB_LW, SB_LBT, SB_COMPACT, SB_SPL
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
 // [2^(15+b), 2^(16+b)) cycles (b = 0 also holds shorter ones, b = 8 longer)
 enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
+// (SC_HIST .. SC_HIST + 8 are the histogram) learning counts: pool scans and
+// the slots they swept, SP paged-row replays and the lane-0 cycles they took
+// (summed over waves; filled in by htm_debug_stamps from SpBufs::dbg)
+enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC };
 
 // ---------------------------------------------------------------------------
 // LDS layout
@@ -346,6 +355,8 @@ __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA
 template <typename E, typename F>
 __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E elig, F f) {
     const uint32_t hwm = t.sh->hwm;
+    COUNT(t, SC_NSCAN, 1);
+    COUNT(t, SC_SCANSLOTS, hwm);
     const uint32_t g = threadIdx.x >> 2, sub = threadIdx.x & 3;
     uint32_t nb = 0;
     for (uint32_t base = 0; base < hwm; base += SC_DEPTH * (TM_NT / 4)) {
@@ -1493,6 +1504,97 @@ __device__ __forceinline__ uint32_t key_slot(unsigned long long k) { return 0xFF
 __device__ __forceinline__ uint32_t key_cic(unsigned long long k) { return (uint32_t)(k >> 32) & 0xFFu; }
 __device__ __forceinline__ uint32_t key_act(unsigned long long k) { return (uint32_t)(k >> 40); }
 
+// ---- nupic::Random draws by a whole wave (learning's wave-0 helpers).
+// The generator (TmSh::rng, rf, rr: glibc random_r TYPE_3, r == f - 3 mod 31)
+// is x[n] = x[n-31] + x[n-3]; buffer slot (f + j) % 31 holds x[n-31+j].  The
+// next 31 values y[j] = x[n+j] = v[j] + (j >= 3 ? y[j-3] : v[28+j]) are a
+// stride-3 inclusive scan of v plus v[28 + j % 3]: four cross-lane adds, the
+// block in lanes 0..30 at once instead of 31 dependent LDS round trips.
+// w_rng_peek returns lane j's upcoming raw draw j (the value rng_raw would
+// return; lanes >= 31: 0) without consuming it, w_rng_commit(k) consumes the
+// first k (<= 31) -- the generator then stands exactly where k rng_raw calls
+// leave it.  Call with every lane of the wave.
+__device__ __forceinline__ uint32_t w_rng_peek(Tm& t, uint32_t& y) {
+    TmSh* sh = t.sh;
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane(sh->rf);
+    uint32_t fj = f + l;
+    fj = fj >= 31u ? fj - 31u : fj;
+    const uint32_t v = l < 31u ? sh->rng[fj < 31u ? fj : 0u] : 0u;
+    uint32_t p = v;
+#pragma unroll
+    for (int d = 3; d < 31; d *= 2) {
+        const uint32_t up = (uint32_t)__shfl_up((int)p, d, 64);
+        if (l >= (uint32_t)d) p += up;
+    }
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 28);
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 29);
+    const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 30);
+    const uint32_t m3 = l % 3u;
+    y = p + (m3 == 0u ? b0 : m3 == 1u ? b1 : b2);
+    return l < 31u ? ((y >> 1) & 0x7fffffffu) : 0u;
+}
+
+__device__ __forceinline__ void w_rng_commit(Tm& t, uint32_t y, uint32_t k) {
+    TmSh* sh = t.sh;
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane(sh->rf);
+    __builtin_amdgcn_wave_barrier();  // every lane has read the state (w_rng_peek)
+    if (l < k) {
+        uint32_t fj = f + l;
+        fj = fj >= 31u ? fj - 31u : fj;
+        sh->rng[fj] = y;
+    }
+    if (l == 0) {
+        const uint32_t nf = (f + k) % 31u;
+        sh->rf = (int32_t)nf;
+        sh->rr = (int32_t)((nf + 28u) % 31u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// _chooseCellsToLearnFrom's sample of n of the m candidates (m > n >= 1):
+// bit i of the result = candidate i chosen.  n == 1: one draw, index
+// getUInt32(m); else candidate i is taken when getUInt32(m - i) < n - taken,
+// until n are taken -- the draws of up to 31 candidates and their residues
+// are computed across the lanes at once, the (cheap) sequential decisions
+// read them lane by lane, and exactly the draws the sequential loop makes
+// are consumed.
+__device__ __forceinline__ uint64_t w_rng_sample(Tm& t, uint32_t m, uint32_t n) {
+    const uint32_t l = (uint32_t)lane_id();
+    uint64_t ch = 0;
+    uint32_t cnt = 0, i0 = 0;
+    for (;;) {
+        uint32_t y;
+        const uint32_t raw = w_rng_peek(t, y);
+        if (n == 1u) {
+            const uint32_t u0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(raw % m));
+            w_rng_commit(t, y, 1u);
+            return 1ull << u0;
+        }
+        const uint32_t i = i0 + l;
+        const uint32_t u = (l < 31u && i < m) ? raw % (m - i) : 0u;
+        const uint32_t lim = m - i0 < 31u ? m - i0 : 31u;
+        uint32_t k = 0;
+        bool done = false;
+        for (uint32_t j = 0; j < lim; j++) {
+            const uint32_t uj = (uint32_t)__builtin_amdgcn_readlane((int)u, (int)j);
+            k = j + 1u;
+            if (uj < n - cnt) {
+                ch |= 1ull << (i0 + j);
+                if (++cnt == n) {
+                    done = true;
+                    break;
+                }
+            }
+        }
+        w_rng_commit(t, y, k);
+        i0 += k;
+        if (done || i0 >= m) return ch;
+    }
+}
+
 struct WUpd {
     uint32_t mask;   // active existing synapse positions
     uint32_t n_new;  // new sources
@@ -1531,24 +1633,7 @@ __device__ __forceinline__ WUpd w_build_update(Tm& t, uint32_t slot, const uint3
     if (m <= (uint32_t)n) {
         chosen = (m == 64) ? ~0ull : ((1ull << m) - 1ull);
     } else {
-        uint64_t ch = 0;
-        if (l == 0) {
-            int32_t f = sh->rf, r = sh->rr;
-            if (n == 1) {
-                ch = 1ull << rng_u32(sh->rng, f, r, m);
-            } else {
-                uint32_t cnt = 0;
-                for (uint32_t i = 0; i < m; i++) {
-                    if (rng_u32(sh->rng, f, r, m - i) < (uint32_t)n - cnt) {
-                        ch |= 1ull << i;
-                        if (++cnt == (uint32_t)n) break;
-                    }
-                }
-            }
-            sh->rf = f;
-            sh->rr = r;
-        }
-        chosen = __shfl(ch, 0, 64);
+        chosen = w_rng_sample(t, m, (uint32_t)n);
     }
     if (ok && ((chosen >> pos) & 1ull)) {
         uint32_t op = (uint32_t)__popcll(chosen & ((1ull << pos) - 1ull));
@@ -1829,9 +1914,12 @@ __device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA
     if (ro || nun == 0) return inSeq;
     wg_clear(t.U, 2 * c.ncol);
     __syncthreads();
+    STAMP(t, SB_LEARN);
     scan_best(t, t.lrnA1, c.min_thr, t.flags);
     __syncthreads();
+    STAMP(t, SB_LSCAN);
     build_cand(t, t.lrnA1);
+    STAMP(t, SB_LEARN);
     const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
     if (wave_id() == 0) {
         for (int a = 0; a < nA; a++) {
@@ -1859,6 +1947,7 @@ __device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA
         }
     }
     __syncthreads();
+    STAMP(t, SB_LW);
     return inSeq;
 }
 
@@ -1871,8 +1960,10 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
     wg_clear(t.lrnP, c.cw);
     wg_clear(t.U, 2 * c.ncol);
     __syncthreads();
+    STAMP(t, SB_LEARN);
     scan_best(t, t.lrnA, c.act_thr, nullptr);
     __syncthreads();
+    STAMP(t, SB_LSCAN);
     const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
     for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
         unsigned long long key = keys[col];
@@ -1881,6 +1972,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
     __syncthreads();
     if (ro) return;
     build_cand(t, t.lrnA);
+    STAMP(t, SB_LEARN);
     if (wave_id() == 0) {
         for (int base = 0; base < c.ncol; base += 64) {
             uint64_t b = __ballot(keys[base + lane_id()] != 0ull);
@@ -1915,6 +2007,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
         }
     }
     __syncthreads();
+    STAMP(t, SB_LW);
 }
 
 // start cells (cell 0) of the given columns into lrnA
@@ -1937,12 +2030,17 @@ __device__ __forceinline__ bool learn_backtrack_from(Tm& t, int start, bool ro) 
     }
     bool inSeq = true;
     for (int off = start; off < numPrev; off++) {
+        STAMP(t, SB_LEARN);
         wg_copy(t.lrnP1, t.lrnP, cw);
         wg_copy(t.lrnA1, t.lrnA, cw);
         __syncthreads();
+        STAMP(t, SB_LBT);
         const uint16_t* pat = lrn_pat(t, off);
         const int len = lrn_len(t, off);
-        if (!ro) process_segment_updates(t, pat, len);
+        if (!ro) {
+            process_segment_updates(t, pat, len);
+            STAMP(t, SB_LUPD);
+        }
         if (off == start) {
             set_start_cells(t, t.lrnA, pat, len);
             inSeq = true;
@@ -2011,7 +2109,9 @@ __device__ __forceinline__ void update_learning(Tm& t) {
     if (sh->ti[1] >= 0)
         for (int a = threadIdx.x; a < sh->nA; a += TM_NT) t.lrnpat[sh->ti[1]][a] = sh->act[a];
     __syncthreads();
+    STAMP(t, SB_LEARN);
     process_segment_updates(t, sh->act, sh->nA);
+    STAMP(t, SB_LUPD);
     if (threadIdx.x == 0) {
         if (sh->pam > 0) sh->pam--;
         sh->lsl++;
@@ -2251,7 +2351,15 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         for (int k = 0; k < HTM_NSTAMP; k++) sh->st_acc[k] = sh->st_cnt[k] = 0;
         sh->st_last = __builtin_amdgcn_s_memtime();
         sh->st_start = sh->st_last;
-        if (sh->st_sp0 && sh->st_sp0 < sh->st_last) sh->st_acc[SB_SP] = sh->st_last - sh->st_sp0;  // the fused SP
+        if (sh->st_sp0 && sh->st_sp0 < sh->st_last) {  // the fused SP: inference part, learning part
+            const uint64_t tl = reinterpret_cast<const SpShared*>(lds + tm_layout(c, LEARN, FROZEN).off_U)->st_t_learn;
+            if (tl > sh->st_sp0 && tl < sh->st_last) {
+                sh->st_acc[SB_SP] = tl - sh->st_sp0;
+                sh->st_acc[SB_SPL] = sh->st_last - tl;
+            } else {
+                sh->st_acc[SB_SP] = sh->st_last - sh->st_sp0;
+            }
+        }
         sh->st_sp0 = 0;
     }
 #endif
@@ -2383,7 +2491,10 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     }
     __syncthreads();
     STAMP(t, SB_LOAD);
-    if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) compact_pool(t);
+    if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) {
+        compact_pool(t);
+        STAMP(t, SB_COMPACT);
+    }
     // ---- BacktrackingTM.compute(input, learn, infer=True)
     update_inference<FROZEN>(t);
     STAMP(t, SB_BT);

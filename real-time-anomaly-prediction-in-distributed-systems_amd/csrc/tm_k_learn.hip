@@ -3,8 +3,15 @@
 // index (HTM_OPT_FROZEN_INDEX 0).  Kernel bodies: tm_core.h.
 #include "tm_core.h"
 
+// waves per SIMD the kernels are compiled for (the LDS layout fits 3
+// workgroups per CU; the register budget decides: 2 -> up to 256 VGPRs)
+#ifndef HTM_LEARN_WAVES
+#define HTM_LEARN_WAVES 2
+#endif
+
 template <bool LEARN>
-__global__ __launch_bounds__(TM_NT) void htm_run_kernel(HTM_RUN_ARGS) {
+__global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_LEARN_WAVES))) void htm_run_kernel(
+    HTM_RUN_ARGS) {
     htm_run_body<LEARN, false, true>(HTM_RUN_PASS);
 }
 

@@ -279,18 +279,23 @@ class HTMEngine:
     def debug_stamps(self) -> dict:
         """Per-phase TM cycle stamps + event counts (diagnostic stamps build only);
         "tail": the same over stream-steps whose TM part took >= 2^18 cycles."""
-        out = (ctypes.c_uint64 * 96)()
+        N = 32
+        out = (ctypes.c_uint64 * (4 * N))()
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
-                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp", "norm"]
-        cnames = ["phase2", "windows", "blocks", "qualifying", "active_cells", "nonzero_cols", "steps"]
+                 "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp", "norm",
+                 "learn_scan", "learn_updates", "learn_wave0", "learn_bt_copy", "compact", "sp_learn"]
+        cnames = {0: "phase2", 1: "windows", 2: "blocks", 3: "qualifying", 4: "active_cells", 5: "nonzero_cols",
+                  6: "steps", 16: "pool_scans", 17: "pool_scan_slots", 18: "sp_row_replays",
+                  19: "sp_row_replay_cycles"}
 
         def part(o):
             return dict(cycles={k: int(out[o + i]) for i, k in enumerate(names)},
-                        counts={k: int(out[o + 24 + i]) for i, k in enumerate(cnames)},
-                        step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[o + 31 + b]) for b in range(9)})
+                        counts={k: int(out[o + N + i]) for i, k in cnames.items()},
+                        step_cycle_hist={f"<2^{16 + b}" if b < 8 else ">=2^23": int(out[o + N + 7 + b])
+                                         for b in range(9)})
         r = part(0)
-        r["tail"] = part(48)
+        r["tail"] = part(2 * N)
         return r
 
     def frozen_index_valid(self) -> bool:

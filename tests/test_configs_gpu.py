@@ -13,6 +13,8 @@ Config 5: the cpu / mem / mean / max response-time aggregate
           (StreamEngine/StreamAggregator.py:101-115) through a 4-field
           MultiEncoder into a 4096-column SP (configs[4]).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -117,6 +119,44 @@ def test_config4_fleet_flush_beside_the_steps(rt, fleet_model, traces):
         o = orc.clone()
         want = np.array([o.step([vals[k, s]], False, False) for k in range(T)], np.float32)
         assert np.array_equal(got[:, s], want), f"stream {s}"
+
+
+def test_config4_fleet_131072_save_resume(rt, fleet_model, traces, tmp_path):
+    """Checkpoint / resume at fleet scale (NetworkModel.py:123-125 saves the
+    network before the step, ModelTesting.py:176 reloads it): a 131,072-stream
+    fleet saved after 40 lockstep steps (deferred writes pending) and loaded
+    back continues bit-exactly like the fleet that was not saved -- every
+    stream's scores, sampled streams' cell states, the shared model's segment
+    records -- and sampled streams equal oracle clones throughout."""
+    model, orc = fleet_model
+    n, T, cut = 131072, 72, 40
+    vals = fleet_inputs(traces, n, T, seed=37)
+    v = torch.tensor(vals, device="cuda")
+    fl = rt.HTMEngine.fleet(model, n, q_capacity=4096)
+    head = np.stack([fl.step(v[k]).cpu().numpy() for k in range(cut)])
+    path = str(tmp_path / "fleet131072.htm")
+    fl.save(path)
+    re = rt.HTMEngine.load(path)
+    assert re.is_fleet and re.n_streams == n
+    a = np.stack([fl.step(v[k]).cpu().numpy() for k in range(cut, T)])
+    b = np.stack([re.step(v[k]).cpu().numpy() for k in range(cut, T)])
+    assert np.array_equal(a, b)
+    fl.status()
+    re.status()
+    for s in (0, 77777, n - 1):
+        sa, sb = fl.tm_states(s), re.tm_states(s)
+        for k in sa:
+            assert np.array_equal(sa[k], sb[k]), (s, k)
+    for region in ("tm_seg_duty", "tm_seg_meta"):  # the shared model: one instance
+        assert np.array_equal(fl.export_state(region, 0, 1), re.export_state(region, 0, 1)), region
+    got = np.concatenate([head, b])
+    for s in (3, 65536 + 11, n - 2):
+        o = orc.clone()
+        want = np.array([o.step([vals[k, s]], False, False) for k in range(T)], np.float32)
+        assert np.array_equal(got[:, s], want), f"stream {s}"
+    re.close()
+    fl.close()
+    os.remove(path)
 
 
 def test_config3_many_fresh_streams_learning(rt, oracle_mod):

@@ -65,11 +65,40 @@ def test_fleet_equals_replicated_engines(rt, model, traces, pid_lists, monkeypat
     fl.status()
 
 
-def test_fleet_refuses_learning_and_save(rt, model, tmp_path):
+def test_fleet_refuses_learning(rt, model):
     fl = rt.HTMEngine.fleet(model, 4)
     with pytest.raises(rt.HtmError):
         fl.set_learning(True, False)
     with pytest.raises(rt.HtmError):  # the pool scan would race on the shared segment records
         fl.use_frozen_index(False)
-    with pytest.raises(rt.HtmError):
-        fl.save(str(tmp_path / "f.htm"))
+
+
+def test_fleet_save_load_round_trip(rt, model, traces, tmp_path):
+    """A fleet saved mid-run (htm_save: the shared model once, every stream's
+    state) loads back as a fleet and continues exactly like the unsaved one;
+    the file holds one model, not one per stream."""
+    n, T = 64, 80
+    rng = np.random.default_rng(23)
+    base = np.asarray(traces["test"][:T], np.float64)
+    v = torch.tensor(np.clip(base[:, None] + rng.integers(-3, 4, size=(T, n)), 0, 100), device="cuda")
+    fl = rt.HTMEngine.fleet(model, n, q_capacity=4096)
+    for k in range(40):
+        fl.step(v[k])
+    path = str(tmp_path / "fleet.htm")
+    fl.save(path)
+    re = rt.HTMEngine.load(path)
+    assert re.is_fleet and re.n_streams == n and not re.sp_learn and not re.tm_learn
+    a = np.stack([fl.step(v[k]).cpu().numpy() for k in range(40, T)])
+    b = np.stack([re.step(v[k]).cpu().numpy() for k in range(40, T)])
+    assert np.array_equal(a, b)
+    for s in (0, n - 1):
+        for k, x in fl.tm_states(s).items():
+            assert np.array_equal(x, re.tm_states(s)[k]), k
+    for region in ("tm_seg_duty", "tm_seg_meta", "sp_perm"):  # the shared model: one instance
+        assert np.array_equal(fl.export_state(region, 0, 1), re.export_state(region, 0, 1)), region
+    # (the header's last 8 bytes count algorithmic bytes: the loaded fleet's
+    # deferred log starts empty, so it logs sets the saved one deduplicated)
+    assert np.array_equal(fl.export_state("tm_header")[:, :-8], re.export_state("tm_header")[:, :-8])
+    import os
+    model_bytes = sum(fl.state_bytes(r) for r in ("sp_perm", "sp_potmask", "sp_connT", "tm_seg_src", "tm_seg_perm"))
+    assert os.path.getsize(path) < 2 * model_bytes + n * 64 * 1024
