@@ -414,6 +414,10 @@ def main():
     ap.add_argument("--seg-capacity", type=int, default=None, help="segment slots per stream")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--profile-every", type=int, default=4,
+                    help="HIP events around every N-th launch of the timed region (HTM_OPT_PROFILE N; a timed "
+                         "event record between dependent launches holds the queue ~12 us, so the roofline's "
+                         "launch time is averaged over a sample: default every 4th)")
     ap.add_argument("--mode", choices=["step", "run"], default="step",
                     help="step (default, the headline): lockstep -- one htm_step per step, every stream "
                          "advances one network.run(1) per step (north_star's real-time stepping); run: the K "
@@ -582,7 +586,7 @@ def main():
     sync()
     c0 = eng.counters()
     if not args.no_profile:
-        eng.profile(True)
+        eng.profile(True, every=args.profile_every if args.mode == "step" else 1)
     # the timed region: K steps bracketed by barrier + synchronize, max over ranks
     dt, _ = timed_replay(eng, vals, scores, C + args.warmup, args.steps, args.mode, args.chunk, gather, gathered,
                          rank, world, dev)
@@ -611,8 +615,10 @@ def main():
         avg_ms = prof["tm_ms"] / launches
         if c3:  # learning: unique bytes (the in-kernel count charges every pool re-scan)
             per_launch = learn_on_bytes(eng, S, (c0["seg_live"] + c1["seg_live"]) / 2) * S * prof["steps"] / launches
-        else:   # frozen inference: the kernel's own count of the index blocks and state it moves
-            per_launch = (c1["tm_bytes"] - c0["tm_bytes"]) / launches
+        else:   # frozen inference: the kernel's own count of the index blocks and state it moves,
+            # over every launch of the timed region (the events sample some of them)
+            all_launches = args.steps if args.mode == "step" else -(-args.steps // args.chunk)
+            per_launch = (c1["tm_bytes"] - c0["tm_bytes"]) / all_launches
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
         traffic, tsrc, k = None, pmc_note, None
         if args.pmc_summary:
@@ -628,7 +634,7 @@ def main():
                 "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
                 "traffic_source": tsrc, "kernel": kernel_name(c3, c4, eng.fused),
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
-                "bytes_per_launch": int(per_launch),
+                "profiled_launches": launches, "bytes_per_launch": int(per_launch),
                 "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
         if c4:
             # a fleet's streams share one model: its index and records are read

@@ -158,7 +158,8 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                   frozen cell->segment forward index; 0: scan the pool */
 #define HTM_OPT_KEEP_PREV 2    /* 1: retain prevPredictedColumns for HTM_OUT_PREV_PRED_COLS */
 #define HTM_OPT_KEEP_OVERLAPS 3 /* 1: retain SP overlaps for HTM_OUT_SP_OVERLAPS */
-#define HTM_OPT_PROFILE 4       /* 1: bracket each step's SP and TM kernels with HIP events */
+#define HTM_OPT_PROFILE 4       /* N >= 1: bracket the SP and TM kernels of every N-th launch with HIP
+                                   events (1: every launch; htm_profile_read averages the sampled ones) */
 #define HTM_OPT_FUSED 5         /* 1 (default): one fused SP+TM kernel per htm_step and per
                                    chunk of htm_run steps (each stream runs its chunk without
                                    waiting for the others); 0: separate SP and TM launches */

@@ -80,7 +80,8 @@ struct htm_engine {
     size_t fx_cap = 0;
     uint64_t* d_counts = nullptr;
     Region regions[HTM_ST_COUNT + 1];
-    int32_t profile = 0;
+    int32_t profile = 0;            // HTM_OPT_PROFILE: 0 off, N: HIP events around every N-th launch
+    uint32_t prof_seq = 0;          // launches since profiling was switched on
     std::vector<hipEvent_t> ev_pool;
     std::vector<int32_t> ev_steps;  // steps covered by each profiled event triple
     std::vector<char> ev_fused;     // the triple's first event is unused (fused launch: no SP kernel)
@@ -121,6 +122,7 @@ static const char* ab_knob(const char* name) {
 
 static int flush_deferred(htm_engine* e, hipStream_t st);
 static int flush_sync(htm_engine* e);
+static int grow_enc(htm_engine* e, size_t steps, hipStream_t st);
 static int densify_conf(htm_engine* e, hipStream_t st);
 
 extern "C" {
@@ -217,6 +219,7 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     d.enc_type = sdr ? HTM_ENC_SCALAR : c.enc_type;
     d.rdse_res = c.rdse_resolution;
     d.rdse_block = (int32_t)(RDSE_HDR_WORDS * 4 + round_up((size_t)HTM_RDSE_BUCKETS * c.enc_w * 2, 16));
+    d.enc_list = (int32_t)round_up((size_t)c.n_fields * c.enc_w + 1, 8);
     d.enc_n = c.enc_n;
     d.enc_w = c.enc_w;
     d.enc_clip = c.enc_clip;
@@ -528,6 +531,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     }
     if (!r) r = check_lds(e->dc);
     if (!r) r = allocate(e);
+    if (!r) r = grow_enc(e, (size_t)e->run_chunk, nullptr);  // RDSE engines: capacity failures show up here
     if (!r && tm_configure_lds(e->dc)) {
         size_t mx = std::max(tm_step_lds_bytes(e->dc, 0, 1),
                              std::max(tm_step_lds_bytes(e->dc, 1, 0), tm_step_lds_bytes(e->dc, 0, 0)));
@@ -535,6 +539,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     }
     if (r) {
         for (void* p : e->allocs) (void)hipFree(p);
+        if (e->sp.enc_in) (void)hipFree(e->sp.enc_in);
         delete e;
         return r;
     }
@@ -615,7 +620,9 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
     else if (opt == HTM_OPT_KEEP_PREV) e->keep_prev = value ? 1 : 0;
     else if (opt == HTM_OPT_KEEP_OVERLAPS) e->keep_overlaps = value ? 1 : 0;
     else if (opt == HTM_OPT_PROFILE) {
-        e->profile = value ? 1 : 0;
+        if (value < 0) return htm_fail(HTM_E_INVALID, "profile: 0 off, N >= 1 every N-th launch");
+        e->profile = value;
+        e->prof_seq = 0;
         e->ev_used = 0;
         e->ev_steps.clear();
         e->ev_fused.clear();
@@ -681,7 +688,7 @@ static int alloc_dlog(htm_engine* e) {
     ALLOC(e->tm.fx_dupto, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
     ALLOC(e->tm.fx_fwork, uint32_t, 4);
-    ALLOC(e->tm.fx_fjobs, uint32_t, S * (size_t)d.fx_dcap);
+    ALLOC(e->tm.fx_fjobs, uint32_t, S * (size_t)d.fx_dcap * (size_t)d.fx_nwin);
     if (e->flush_prio) {
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -702,16 +709,17 @@ static int alloc_dlog(htm_engine* e) {
 // the ring's free slots and never read the segment records it writes).
 static int flush_async(htm_engine* e, hipStream_t st) {
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
-    if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
     if (e->flush_mode == 1 || st == e->fstream) {
-        if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st))
+        // on the stream of the steps, after them: the bound is fx_dn itself
+        if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1))
             return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
         e->defer_steps = 0;
         return HTM_OK;
     }
+    if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
     HIP_TRY(hipEventRecord(e->ev_logged, st));
     HIP_TRY(hipStreamWaitEvent(e->fstream, e->ev_logged, 0));
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, e->fstream))
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, e->fstream, 0))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(e->ev_flushed, e->fstream));
     e->defer_steps = 0;
@@ -729,7 +737,7 @@ static int flush_deferred(htm_engine* e, hipStream_t st) {
         e->flush_pending = false;
     }
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
-    if (launch_tm_fx_snap(e->tm, e->n, st) || launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st))
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     e->defer_steps = 0;
     return HTM_OK;
@@ -791,6 +799,15 @@ static int build_fx(htm_engine* e, hipStream_t st) {
 
 extern "C" {
 
+// HTM_OPT_PROFILE N: the events bracket every N-th launch (a timed event
+// record between two dependent launches holds the queue ~12 us -- measured in
+// a 20-step lockstep trace, profiles/r04_b -- so sampling keeps the timed
+// region close to the unprofiled one; the average is over the sampled launches)
+static bool profiled_launch(htm_engine* e) {
+    if (!e->profile) return false;
+    return e->prof_seq++ % (uint32_t)e->profile == 0;
+}
+
 static int next_events(htm_engine* e, hipEvent_t* ev, int32_t steps) {
     // three events per profiled step: before SP, between SP and TM, after TM
     while (e->ev_pool.size() < e->ev_used + 3) {
@@ -827,20 +844,29 @@ static int prepare_step(htm_engine* e, hipStream_t st, int* frozen) {
 }
 
 // RDSE engines: the encoder kernel runs the streams' encoders through the
-// launch's n_steps records first (their buffer grows to the longest launch).
+// launch's n_steps records first.  Their lists (count + n_fields * enc_w bits,
+// DevCfg::enc_list words per stream-step) are allocated at creation for
+// run_chunk steps (the longest fused launch of htm_run); a caller that raises
+// run_chunk grows the buffer (synchronising) on the next longer launch.
+static int grow_enc(htm_engine* e, size_t steps, hipStream_t st) {
+    if (e->dc.enc_type != HTM_ENC_RDSE || steps <= e->enc_cap) return HTM_OK;
+    const size_t per = (size_t)e->n * e->dc.enc_list * 2;
+    if (e->sp.enc_in) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipFree(e->sp.enc_in));
+        e->bytes -= e->enc_cap * per;
+        e->sp.enc_in = nullptr;
+        e->enc_cap = 0;
+    }
+    HIP_TRY(hipMalloc(&e->sp.enc_in, steps * per));
+    e->enc_cap = steps;
+    e->bytes += e->enc_cap * per;
+    return HTM_OK;
+}
+
 static int encode_rdse(htm_engine* e, const double* d_values, int32_t n_steps, hipStream_t st) {
     if (e->dc.enc_type != HTM_ENC_RDSE) return HTM_OK;
-    if ((size_t)n_steps > e->enc_cap) {
-        if (e->sp.enc_in) {
-            HIP_TRY(hipStreamSynchronize(st));
-            HIP_TRY(hipFree(e->sp.enc_in));
-            e->bytes -= e->enc_cap * (size_t)e->n * ENC_LIST * 2;
-            e->sp.enc_in = nullptr;
-        }
-        HIP_TRY(hipMalloc(&e->sp.enc_in, (size_t)n_steps * e->n * ENC_LIST * 2));
-        e->enc_cap = (size_t)n_steps;
-        e->bytes += e->enc_cap * (size_t)e->n * ENC_LIST * 2;
-    }
+    if (int r = grow_enc(e, (size_t)n_steps, st)) return r;
     if (launch_rdse_encode(e->dc, e->sp, d_values, n_steps, e->n, st)) return htm_fail(HTM_E_HIP, "rdse encode launch");
     return HTM_OK;
 }
@@ -849,7 +875,8 @@ static int encode_rdse(htm_engine* e, const double* d_values, int32_t n_steps, h
 static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, float* d_scores, hipStream_t st,
                      int frozen) {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    if (e->profile) {
+    const bool prof = profiled_launch(e);
+    if (prof) {
         int r = next_events(e, ev, n_steps);
         if (r) return r;
         // one event before and one after the fused kernel (an event record is
@@ -876,7 +903,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     e->conf_packed = true;
-    if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
+    if (prof) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
     if (defer && ++e->defer_steps >= std::min(e->flush_every ? e->flush_every : FLUSH_EVERY, e->dc.fx_dcap / 2)) {
         int r = flush_async(e, st);  // beside the next steps
         if (r) return r;
@@ -889,7 +916,8 @@ static int step_unfused(htm_engine* e, const double* d_values, const uint32_t* d
                         hipStream_t st, int frozen) {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     int r;
-    if (e->profile) {
+    const bool prof = profiled_launch(e);
+    if (prof) {
         r = next_events(e, ev, 1);
         if (r) return r;
         HIP_TRY(hipEventRecord(ev[0], st));
@@ -902,13 +930,13 @@ static int step_unfused(htm_engine* e, const double* d_values, const uint32_t* d
         // prevPredictedColumns (nonzero colConfidence before compute)
         if (launch_prev_pred(e->dc, e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "prev_pred launch");
     }
-    if (e->profile) HIP_TRY(hipEventRecord(ev[1], st));
+    if (prof) HIP_TRY(hipEventRecord(ev[1], st));
     TmBufs tb = e->tm;
     tb.fx_dlog = nullptr;  // (deferred duty writes: fused lockstep launches only)
     if (launch_tm_step(e->dc, tb, e->sp, d_scores, e->tm_learn, frozen, e->n, st))
         return htm_fail(HTM_E_HIP, "tm_step launch: %s", hipGetErrorString(hipGetLastError()));
     e->conf_packed = true;
-    if (e->profile) HIP_TRY(hipEventRecord(ev[2], st));
+    if (prof) HIP_TRY(hipEventRecord(ev[2], st));
     return HTM_OK;
 }
 

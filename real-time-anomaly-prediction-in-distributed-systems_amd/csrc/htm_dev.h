@@ -82,7 +82,8 @@ struct DevCfg {
     int32_t sp_paged;                     // 1: rows from SpBufs::pool on first change, else init values
     int32_t n_ckpt;                       // nupic::Random checkpoints per stream (ncol / SP_CKPT_COLS)
     int32_t pool_stride;                  // floats per pool row: n_potential rounded up to 128 B
-    int32_t pad0;
+    int32_t enc_list;                     // u16 words per (step, stream) encoded input list (RDSE):
+                                          // count + n_fields * enc_w, rounded up to 8
     uint64_t pool_rows;                   // rows in SpBufs::pool
     // boosting (updateBoostFactorsGlobal_): strength (0: factors stay 1.0, the
     // integer inhibition path) and the target density numActive / area
@@ -99,7 +100,6 @@ struct DevCfg {
 // 16-byte loads)
 __host__ __device__ inline size_t fx_dstride(const DevCfg& c) { return ((size_t)c.max_act_cells + 7) & ~(size_t)7; }
 
-#define ENC_LIST 128        // u16 words per (step, stream) encoded input list: count, then the bits
 #define RDSE_HDR_WORDS 64   // int32 words of an RDSE field header (HTM_ST_ENC_RDSE)
 
 #define SP_CKPT_COLS 8      // columns per SP-initialisation checkpoint (paged permanences)
@@ -132,7 +132,7 @@ struct SpBufs {
     // RDSE encoders (DevCfg::enc_type == HTM_ENC_RDSE): per stream, per field
     // a block of rdse_block bytes (header int32[RDSE_HDR_WORDS], then the
     // int16 [HTM_RDSE_BUCKETS][enc_w] bucket map); the encoded active-input
-    // lists of the steps of one launch [steps][S][ENC_LIST] (word 0 = count);
+    // lists of the steps of one launch [steps][S][enc_list] (word 0 = count);
     // the last record's bucket per field (HTM_OUT_BUCKETS)
     uint8_t* rdse;
     uint16_t* enc_in;
@@ -205,7 +205,8 @@ struct TmBufs {
                                    //     advances fx_dflushed to exactly that (never to a later snapshot)
     uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
     uint32_t* fx_fwork;            // [4] flush job counter, error flags (FX_ERR_*), jobs
-    uint32_t* fx_fjobs;            // [S * fx_dcap] the running flush's entries (stream * fx_dcap + ring slot)
+    uint32_t* fx_fjobs;            // [S * fx_dcap * fx_nwin] the running flush's jobs:
+                                   //     (stream * fx_dcap + ring slot) * fx_nwin + rank window
 };
 
 // deferred-log flush error flags (fx_fwork[1]; htm_status / htm_counters)
@@ -449,7 +450,7 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
                    uint32_t* wq, int unit_steps, hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
-int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st);
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn);
 int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

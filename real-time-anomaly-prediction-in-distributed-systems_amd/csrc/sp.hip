@@ -446,7 +446,7 @@ __global__ void rdse_encode_kernel(DevCfg c, SpBufs b, const double* values, int
     const int nf = c.n_fields, w = c.enc_w;
     uint32_t bin[64];  // newRep as a bitmap (n <= 2048 bits)
     for (int k = 0; k < n_steps; k++) {
-        uint16_t* out = b.enc_in + ((size_t)k * n_streams + s) * ENC_LIST;
+        uint16_t* out = b.enc_in + ((size_t)k * n_streams + s) * c.enc_list;
         int cnt = 0;
         for (int f = 0; f < nf; f++) {
             const double x = values[((size_t)k * n_streams + s) * nf + f];

@@ -479,10 +479,27 @@ __device__ __forceinline__ void sp_replay_init(const SpInitCfg& c, int s, int co
 // without its per-draw lane-0 bookkeeping: the generator runs wave-uniformly
 // (its 31 words are the same in every lane, in scalar registers), lane
 // k % 64 keeps the four draws of permanence rank k, and each 64 ranks are
-// computed and stored by the 64 lanes at once (coalesced).  Out of line, so
-// the replay does not weigh on the fused kernels' register budget.  Call with
-// every lane of the wave.
-static __device__ __attribute__((noinline)) void sp_regen_row(SpInitCfg c, int s, int col, float* row) {
+// computed and stored by the 64 lanes at once (coalesced).  Inlined: as a
+// call its arguments would arrive in VGPRs and the generator's state and
+// control flow would stay per-lane (exec-masked); inlined, the compiler keeps
+// them in scalar registers (the kernels' VGPR counts are unchanged).  Call
+// with every lane of the wave.
+static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int col_, float* row_) {
+    // wave-uniform for the compiler (pointers stay as passed: a readfirstlane'd
+    // pointer trips LLVM's gfx950 verifier, a src_shared_base compare -- the
+    // values loaded through them are made uniform where they are read)
+    SpInitCfg c = c_;
+    c.nin = __builtin_amdgcn_readfirstlane(c_.nin);
+    c.nin_pad = __builtin_amdgcn_readfirstlane(c_.nin_pad);
+    c.ncol = __builtin_amdgcn_readfirstlane(c_.ncol);
+    c.n_potential = __builtin_amdgcn_readfirstlane(c_.n_potential);
+    c.n_ckpt = __builtin_amdgcn_readfirstlane(c_.n_ckpt);
+    c.sp_conn = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c_.sp_conn)));
+    c.sp_trim = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c_.sp_trim)));
+    c.sp_conn_thr = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c_.sp_conn_thr)));
+    const int s = __builtin_amdgcn_readfirstlane(s_), col = __builtin_amdgcn_readfirstlane(col_);
+    float* const row = row_;  // (stores only: per-lane addresses are fine; a readfirstlane'd
+                              // pointer trips LLVM's gfx950 verifier, src_shared_base compare)
     const uint32_t l = (uint32_t)lane_id();
     const int pw = c.nin_pad >> 5;
     const int g0 = col - col % SP_CKPT_COLS;
@@ -658,7 +675,7 @@ __device__ __forceinline__ void sp_count_iteration(const SpBufs& b, int s, SH& s
 
 // Input stage, encoder: RecordSensor -> MultiEncoder.encodeIntoArray.  A
 // ScalarEncoder is computed here; RDSE engines read the list
-// rdse_encode_kernel made for this step (enc: [S][ENC_LIST], count first).
+// rdse_encode_kernel made for this step (enc: [S][enc_list], count first).
 template <bool LEARN>
 __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, const double* values, int s,
                                               SpShared& sh, const uint16_t* enc = nullptr) {
@@ -667,7 +684,7 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
     if (t == 0) {
         int n = 0;
         if (enc) {
-            const uint16_t* e = enc + (size_t)s * ENC_LIST;
+            const uint16_t* e = enc + (size_t)s * c.enc_list;
             n = e[0];
             for (int k = 0; k < n; k++) sh.act_inputs[k] = e[1 + k];
         } else {

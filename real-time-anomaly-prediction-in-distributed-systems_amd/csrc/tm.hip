@@ -349,14 +349,18 @@ int tm_configure_lds(const DevCfg& c) {
 // only to that flush's fx_dupto; a stale read leaves it fewer free slots,
 // never more).  Every job is checked before use (FX_ERR_JOB): a bad one is
 // skipped and flagged, never dereferenced.
+// A job is one rank window of one logged entry: the windows of a bursting set
+// (the longest jobs) run on separate workgroups, so a flush -- the one that
+// ends a timed region above all -- takes about one window's counting.
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
-    const uint32_t dcap = (uint32_t)c.fx_dcap;
+    const uint32_t dcap = (uint32_t)c.fx_dcap, nwin = (uint32_t)c.fx_nwin;
+    const uint32_t cap = (uint32_t)n * dcap * nwin;
     uint32_t total = b.fx_fwork[2];  // the job list (tm_fx_jobs_kernel, the launch before)
-    if (total > (uint32_t)n * dcap) {
+    if (total > cap) {
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
-        total = (uint32_t)n * dcap;
+        total = cap;
     }
     for (;;) {
         __syncthreads();
@@ -364,7 +368,9 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         __syncthreads();
         const uint32_t jj = __builtin_amdgcn_readfirstlane(job);
         if (jj >= total) break;
-        const uint32_t j = __builtin_amdgcn_readfirstlane(b.fx_fjobs[jj]);  // stream * dcap + ring slot
+        // (stream * dcap + ring slot) * nwin + window
+        const uint32_t jw = __builtin_amdgcn_readfirstlane(b.fx_fjobs[jj]);
+        const uint32_t win = jw % nwin, j = jw / nwin;
         const uint32_t su = j / dcap;
         const uint32_t i = j % dcap;
         const uint32_t len0 = su < (uint32_t)n ? (uint32_t)b.fx_dlen[(size_t)su * dcap + i] : 0xFFFFFFFFu;
@@ -393,7 +399,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
             if (cell < (uint32_t)c.ncells) atomicOr(&t.infA[cell >> 5], 1u << (cell & 31));
         }
         __syncthreads();
-        collect_frozen(t, c.act_thr, FX_WIN);
+        collect_frozen(t, c.act_thr, FX_WIN, (int)win);
         __syncthreads();
         if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)c.q_cap) {
             atomicOr(&b.fx_fwork[1], FX_ERR_QCAP);  // qualifying-list overflow, as in the step (htm_status)
@@ -415,11 +421,13 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
 // flush slower than that) moves fx_dsnap, not what this flush completes --
 // its done kernel advances fx_dflushed to fx_dupto, so no entry is marked
 // flushed without having been replayed.  One workgroup per stream.
-__global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n) {
+// from_dn: the flush runs on the step stream after the steps (nothing appends
+// meanwhile), so the bound is fx_dn itself -- no snapshot launch.
+__global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n, int from_dn) {
     __shared__ uint32_t hsh[64], len[64], keep[64];
     const int s = blockIdx.x;
     const uint32_t dcap = (uint32_t)c.fx_dcap;
-    const uint32_t f = b.fx_dflushed[s], u = b.fx_dsnap[s], p = u - f;
+    const uint32_t f = b.fx_dflushed[s], u = from_dn ? b.fx_dn[s] : b.fx_dsnap[s], p = u - f;
     // the ring invariant: fx_dflushed <= fx_dsnap <= fx_dflushed + fx_dcap
     // (a step appends only while fewer than fx_dcap entries are unflushed)
     const bool bad = p > dcap || dcap > 64u;
@@ -475,15 +483,22 @@ __global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        // one job per (kept entry, rank window of the stream's model)
+        const uint32_t nwin = (uint32_t)c.fx_nwin, W = (uint32_t)c.fx_win;
+        const uint32_t nr = b.fx_nr[model_stream(c, s)];
+        uint32_t nw = (nr + W - 1u) / W;
+        nw = nw < nwin ? nw : nwin;
         uint32_t m = 0;
         for (uint32_t i = 0; i < p; i++) m += keep[i];
-        uint32_t base = atomicAdd(&b.fx_fwork[2], m);
-        const uint32_t cap = (uint32_t)n * dcap;
+        uint32_t base = atomicAdd(&b.fx_fwork[2], m * nw);
+        const uint32_t cap = (uint32_t)n * dcap * nwin;
         for (uint32_t i = 0; i < p; i++) {
             if (!keep[i]) continue;
-            if (base < cap) b.fx_fjobs[base] = (uint32_t)s * dcap + (f + i) % dcap;
-            else atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
-            base++;
+            const uint32_t e = (uint32_t)s * dcap + (f + i) % dcap;
+            for (uint32_t w = 0; w < nw; w++, base++) {
+                if (base < cap) b.fx_fjobs[base] = e * nwin + w;
+                else atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
+            }
         }
     }
 }
@@ -510,14 +525,14 @@ int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st) {
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn) {
     if (n <= 0 || !b.fx_dlog) return 0;
     const size_t lds = tm_step_lds_bytes(c, 0, 1);
-    const int total = n * c.fx_dcap;
+    const int total = n * c.fx_dcap * c.fx_nwin;
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
-    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3(n), dim3(256), 0, st, c, b, n);
+    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3(n), dim3(256), 0, st, c, b, n, from_dn);
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;

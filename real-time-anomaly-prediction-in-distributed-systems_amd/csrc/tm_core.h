@@ -571,7 +571,8 @@ __device__ __forceinline__ void wg_clear4(uint32_t* p, uint32_t nquads) {
 // list a pid-only call left in U)
 enum { FX_ALL = 0, FX_PID = 1, FX_WIN = 2, FX_WIN_REUSE = 3 };
 
-__device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL) {
+// win >= 0 (FX_WIN only): count that one rank window (the flush's per-window jobs)
+__device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL, int win = -1) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const uint32_t W = (uint32_t)c.fx_win;
@@ -639,8 +640,8 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
             }
         }
     };
-    const int w_first = (pid_ok && t.np > 0 && mode != FX_WIN && mode != FX_WIN_REUSE) ? -1 : 0;
-    const int w_end = mode == FX_PID ? 0 : (int)nw;
+    const int w_first = (pid_ok && t.np > 0 && mode != FX_WIN && mode != FX_WIN_REUSE) ? -1 : win >= 0 ? win : 0;
+    const int w_end = mode == FX_PID ? 0 : win >= 0 ? (win < (int)nw ? win + 1 : win) : (int)nw;
     if (w_first < w_end) load_offsets(w_first);
     for (int w = w_first; w < w_end; w++) {
         // list of (active cell k, pass w): block range [fxoff[idx], fxoff[idx + 1])
@@ -1621,8 +1622,8 @@ __device__ __forceinline__ WUpd w_build_update(Tm& t, uint32_t slot, const uint3
     const int ncand = sh->ncand;
     uint32_t cv = l < ncand ? sh->cand[l] : 0xFFFFFFFEu;
     bool ok = l < ncand;
-    for (uint32_t j = 0; j < nsyn; j++) {
-        uint32_t sj = __shfl(mysrc, (int)j, 64);
+    for (uint32_t j = 0; j < nsyn; j++) {  // (j uniform: a register read, not an LDS permute)
+        const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)mysrc, (int)j);
         if (cv == sj) ok = false;
     }
     uint64_t keep = __ballot(ok);
@@ -1688,9 +1689,9 @@ __device__ __forceinline__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t 
         const uint32_t numToFree = nsyn + n_new - (uint32_t)c.max_syn;
         uint32_t rin = 0, rac = 0;
         for (int k = 0; k < 32; k++) {
-            float pk = __shfl(p, k, 64);
-            int ik = __shfl((int)inact, k, 64);
-            int ak = __shfl((int)isact, k, 64);
+            const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), k));
+            const int ik = __builtin_amdgcn_readlane((int)inact, k);
+            const int ak = __builtin_amdgcn_readlane((int)isact, k);
             bool lt = (pk < p) || (pk == p && k < l);
             if (ik && lt) rin++;
             if (ak && lt) rac++;
@@ -1810,7 +1811,7 @@ __device__ __forceinline__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) 
             sh->rf = f;
             sh->rr = r;
         }
-        idx = __shfl(idx, 0, 64);
+        idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
         // position of the idx-th set bit of b
         uint64_t x = b;
         for (uint32_t k = 0; k < idx; k++) x &= x - 1ull;
@@ -2699,7 +2700,7 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
             k = k0;
         }
         const double* v = values + (size_t)k * c.n_streams * c.n_fields;
-        const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? sp.enc_in + (size_t)k * c.n_streams * ENC_LIST : nullptr;
+        const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? sp.enc_in + (size_t)k * c.n_streams * c.enc_list : nullptr;
 #ifdef HTM_STAMPS
         if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
 #endif

@@ -245,9 +245,10 @@ class HTMEngine:
         """Paged SP permanences: pool rows handed out (0 for a dense engine)."""
         return int(self._L.htm_sp_perm_rows_used(self.h))
 
-    def profile(self, on: bool):
-        """Bracket every step's SP and TM kernels with HIP events."""
-        self.set_option(_lib.OPT_PROFILE, int(on))
+    def profile(self, on, every: int = 1):
+        """Bracket the SP and TM kernels of every `every`-th launch with HIP
+        events (profile_read averages the sampled launches)."""
+        self.set_option(_lib.OPT_PROFILE, int(every) if on else 0)
 
     def profile_read(self) -> dict:
         """{sp_ms, tm_ms (fused launches: SP+TM), steps covered, launches}."""
