@@ -428,7 +428,7 @@ static int allocate(htm_engine* e) {
     ALLOC(e->d_counts, uint64_t, S);
 #ifdef HTM_STAMPS
     ALLOC(e->tm.dbg, uint64_t, S * 4 * HTM_NSTAMP);
-    ALLOC(e->sp.dbg, uint64_t, S * 2);
+    ALLOC(e->sp.dbg, uint64_t, S * 4);
 #endif
     e->tm.fx_ent = nullptr;
     // region table for export / import / save / load / replicate
@@ -1039,15 +1039,14 @@ int htm_debug_stamps(htm_engine* e, uint64_t* out128) {
     if (!e->tm.dbg) return htm_fail(HTM_E_STATE, "not a stamps build (HTM_STAMPS)");
     HIP_TRY(hipDeviceSynchronize());
     const int W = 4 * HTM_NSTAMP;
-    std::vector<uint64_t> h((size_t)e->n * W), r((size_t)e->n * 2);
+    std::vector<uint64_t> h((size_t)e->n * W), r((size_t)e->n * 4);
     HIP_TRY(hipMemcpy(h.data(), e->tm.dbg, h.size() * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(r.data(), e->sp.dbg, r.size() * 8, hipMemcpyDeviceToHost));
     for (int k = 0; k < W; k++) out128[k] = 0;
     for (int s = 0; s < e->n; s++) {
         for (int k = 0; k < W; k++) out128[k] += h[(size_t)s * W + k];
         // SP paged-row replays (not attributable to tail steps)
-        out128[HTM_NSTAMP + SC_REPLAY_IDX] += r[(size_t)s * 2];
-        out128[HTM_NSTAMP + SC_REPLAY_IDX + 1] += r[(size_t)s * 2 + 1];
+        for (int k = 0; k < 4; k++) out128[HTM_NSTAMP + SC_REPLAY_IDX + k] += r[(size_t)s * 4 + k];
     }
     HIP_TRY(hipMemset(e->tm.dbg, 0, h.size() * 8));
     HIP_TRY(hipMemset(e->sp.dbg, 0, r.size() * 8));

@@ -138,7 +138,8 @@ struct SpBufs {
     uint16_t* enc_in;
     int32_t* enc_bucket;  // [S][4]
     uint64_t* rdse_seeds; // [S] RDSE seed per stream
-    uint64_t* dbg;        // [S][2] paged-row replays and their lane-0 cycles (HTM_STAMPS builds only, else null)
+    uint64_t* dbg;        // [S][4] paged-row replays, their cycles, of which sampling-draw count and block
+                          // skip (HTM_STAMPS builds only, else null)
 };
 
 struct TmBufs {

@@ -475,16 +475,23 @@ __device__ __forceinline__ void sp_replay_init(const SpInitCfg& c, int s, int co
 }
 
 // The initial permanences of column col of stream s into a fresh pool row,
-// replayed by the whole wave -- sp_replay_init's draws in the same order,
-// without its per-draw lane-0 bookkeeping: the generator runs wave-uniformly
-// (its 31 words are the same in every lane, in scalar registers), lane
-// k % 64 keeps the four draws of permanence rank k, and each 64 ranks are
-// computed and stored by the 64 lanes at once (coalesced).  Inlined: as a
-// call its arguments would arrive in VGPRs and the generator's state and
-// control flow would stay per-lane (exec-masked); inlined, the compiler keeps
-// them in scalar registers (the kernels' VGPR counts are unchanged).  Call
+// replayed by the whole wave -- sp_replay_init's draws, in the same order.
+// The draws the column skips (the group's earlier columns, its own sampling
+// draws) advance the generator in whole 31-draw blocks, wave-uniformly in
+// scalar registers.  The column's own draws, with an LDS scratch `buf` (512
+// words, the wave's share of the SP's overlap planes, free while adapting):
+// the generator moves into the lanes (lane j holds the window word j,
+// x[n-31+j]) and each block of 31 draws is one stride-3 scan across the lanes
+// (y[j] = v[j] + (j >= 3 ? y[j-3] : v[28+j])), written to buf in one store;
+// every 256 draws the 64 lanes convert 64 permanences at once and store them
+// coalesced (double-buffered: a block that crosses a round boundary writes
+// the other half).  Without a scratch the draws go one by one (lane k % 64
+// keeps rank k's four).  Inlined: as a call its arguments would arrive in
+// VGPRs and the scalar control flow would stay per-lane (exec-masked).  Call
 // with every lane of the wave.
-static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int col_, float* row_) {
+template <bool LDSBUF>
+static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int col_, float* row_, uint32_t* buf,
+                                                    unsigned long long* dbg = nullptr) {
     // wave-uniform for the compiler (pointers stay as passed: a readfirstlane'd
     // pointer trips LLVM's gfx950 verifier, a src_shared_base compare -- the
     // values loaded through them are made uniform where they are read)
@@ -508,12 +515,99 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
     const uint32_t npd = 4u * npot;
     // sampling draws of the group's columns g0..col, one lane each
     uint32_t myd = 0;
+#ifdef HTM_STAMPS
+    const uint64_t ts0_ = __builtin_amdgcn_s_memtime();
+#endif
     if (l < (uint32_t)SP_CKPT_COLS && g0 + (int)l <= col) myd = sp_sample_draws(c, pot + (size_t)(g0 + (int)l) * pw, g0 + (int)l);
     uint32_t sk = 0;  // draws to discard before the column's first permanence draw (< 2^31)
     for (int k = 0; k < col - g0; k++) sk += (uint32_t)__builtin_amdgcn_readlane((int)myd, k) + npd;
     sk += (uint32_t)__builtin_amdgcn_readlane((int)myd, col - g0);
     const uint32_t* ck = c.ckpt + ((size_t)s * c.n_ckpt + (size_t)(g0 / SP_CKPT_COLS)) * SP_CKPT_WORDS;
-    uint32_t i = 0;                    // the column's draws taken so far
+#ifdef HTM_STAMPS
+    const uint64_t ts1_ = __builtin_amdgcn_s_memtime();
+    auto stamp_gen = [&]() {  // sampling-draw count, then the whole-block skip
+        if (dbg && l == 0) {
+            const uint64_t ts2_ = __builtin_amdgcn_s_memtime();
+            atomicAdd(&dbg[0], (unsigned long long)(ts1_ - ts0_));
+            atomicAdd(&dbg[1], (unsigned long long)(ts2_ - ts1_));
+        }
+    };
+#endif
+    uint32_t i = 0;  // the column's draws taken so far
+    const uint32_t pend = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[31]);
+    if constexpr (LDSBUF) {
+        // ---- LDS path (an explicit LDS pointer: generic accesses make LLVM
+        // version the code on an is-shared test whose compare trips the gfx950
+        // verifier).  Rounds converted so far; round r = draws [256 r, 256 r + 256)
+        typedef __attribute__((address_space(3))) uint32_t lds_u32;
+        lds_u32* const lb = (lds_u32*)buf;
+        uint32_t rdone = 0;
+        auto convert = [&](uint32_t r) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t k = r * 64u + l;
+            if (k < npot) {
+                const lds_u32* q = lb + ((r & 1u) << 8) + 4u * l;
+                bool isconn;
+                row[k] = sp_init_value(c, q[0], q[1], q[2], q[3], isconn);
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+        auto rounds = [&]() {  // convert every complete round (and the last partial one)
+            const uint32_t have = i < npd ? i : npd;
+            while (rdone < (have >> 8)) convert(rdone++);
+            if (have == npd && (npd & 255u) && rdone == (npd >> 8)) convert(rdone++);
+        };
+        // the checkpoint block's undelivered draws, one by one (lane 0 writes)
+        for (uint32_t j = pend; j < 31u && i < npd; j++) {
+            const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[32 + j]);
+            if (sk) {
+                sk--;
+                continue;
+            }
+            if (l == 0) lb[i & 511u] = d;
+            i++;
+        }
+        rounds();
+        // whole blocks to skip: the scalar generator
+        uint32_t st[31];
+#pragma unroll
+        for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[j]);
+        while (sk >= 31u && i < npd) {
+#pragma unroll
+            for (int j = 0; j < 31; j++) st[(3 + j) % 31] += st[j];
+            sk -= 31u;
+        }
+#ifdef HTM_STAMPS
+        stamp_gen();
+#endif
+        // the generator into the lanes: window word j = st[(3 + j) % 31]
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 31; j++) v = l == (uint32_t)j ? st[(3 + j) % 31] : v;
+        const uint32_t m3 = l % 3u;
+        while (i < npd) {
+            uint32_t p = v;
+#pragma unroll
+            for (int d = 3; d < 31; d *= 2) {
+                const uint32_t up = (uint32_t)__shfl_up((int)p, d, 64);
+                if (l >= (uint32_t)d) p += up;
+            }
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 28);
+            const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 29);
+            const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 30);
+            v = p + (m3 == 0u ? b0 : m3 == 1u ? b1 : b2);  // the next window = this block's values
+            // block draw j (lanes < 31): skipped while j < sk, else column draw i + j - sk
+            if (l < 31u && l >= sk && i + (l - sk) < npd) lb[(i + (l - sk)) & 511u] = (v >> 1) & 0x7fffffffu;
+            i += 31u - sk;
+            sk = 0;
+            rounds();
+        }
+        rounds();
+        return;
+    } else {
+    // ---- one draw at a time (no scratch)
     uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;  // this lane's draws of its current rank
     // one draw: discarded, or the next of the column (true when the column is complete)
     auto take = [&](uint32_t raw) -> bool {
@@ -541,11 +635,13 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
     };
     // draws the checkpoint's block had generated but not handed out yet
     bool done = false;
-    const uint32_t pend = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[31]);
     for (uint32_t j = pend; j < 31u && !done; j++) done = take((uint32_t)__builtin_amdgcn_readfirstlane((int)ck[32 + j]));
     uint32_t st[31];
 #pragma unroll
     for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[j]);
+#ifdef HTM_STAMPS
+    bool gen_ = false;
+#endif
     while (!done) {
         if (sk >= 31u) {
 #pragma unroll
@@ -553,6 +649,12 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
             sk -= 31u;
             continue;
         }
+#ifdef HTM_STAMPS
+        if (!gen_) {
+            gen_ = true;
+            stamp_gen();
+        }
+#endif
 #pragma unroll
         for (int j = 0; j < 31; j++) {
             const int f = (3 + j) % 31;
@@ -560,14 +662,16 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
             if (!done) done = take((st[f] >> 1) & 0x7fffffffu);
         }
     }
+    }
 }
 
 // Permanence row of column col of stream s (wave-uniform; every lane of the
 // wave calls it).  Paged engines hand a column a pool row on its first change
 // (lane 0 regenerates the initial values into it); null when the pool is
 // exhausted (flagged SP_ERR_POOL: the update is dropped, results invalid).
-template <bool PAGED_OK>
-__device__ __forceinline__ float* sp_perm_row(const DevCfg& c, const SpBufs& b, int s, int col) {
+template <bool PAGED_OK, bool LDSBUF = false>
+__device__ __forceinline__ float* sp_perm_row(const DevCfg& c, const SpBufs& b, int s, int col,
+                                              uint32_t* scratch = nullptr) {
     const size_t ms = (size_t)model_stream(c, s);
     if (!PAGED_OK || !c.sp_paged) return b.perm + (ms * c.ncol + col) * c.n_potential;
     uint32_t r = 0, fresh = 0;
@@ -593,13 +697,16 @@ __device__ __forceinline__ float* sp_perm_row(const DevCfg& c, const SpBufs& b, 
 #ifdef HTM_STAMPS
         const uint64_t t0_ = __builtin_amdgcn_s_memtime();
 #endif
-        sp_regen_row(sp_init_cfg(c, b), (int)ms, col, b.pool + (size_t)r * c.pool_stride);
 #ifdef HTM_STAMPS
+        sp_regen_row<LDSBUF>(sp_init_cfg(c, b), (int)ms, col, b.pool + (size_t)r * c.pool_stride, scratch,
+                             b.dbg ? reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 4 + 2]) : nullptr);
         if (b.dbg && lane_id() == 0) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 2]), 1ull);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 2 + 1]),
+            atomicAdd(reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 4]), 1ull);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&b.dbg[(size_t)s * 4 + 1]),
                       (unsigned long long)(__builtin_amdgcn_s_memtime() - t0_));
         }
+#else
+        sp_regen_row<LDSBUF>(sp_init_cfg(c, b), (int)ms, col, b.pool + (size_t)r * c.pool_stride, scratch);
 #endif
         if (lane_id() == 0) *slot = r;
         __threadfence();
@@ -625,13 +732,14 @@ __device__ __forceinline__ float sp_update_perm(const DevCfg& c, float p, bool r
 // One wave adapts one column: lane l owns inputs [8l, 8l+8) of each 512-bit
 // chunk of the potential mask.  mode 0: adaptSynapses_ (+inc/-dec by input),
 // mode 1: bumpUpWeakColumns_ (+synPermBelowStimulusInc, no raise).
-template <bool PAGED_OK>
-__device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b, int s, int col, const uint32_t* in_bits, int mode) {
+template <bool PAGED_OK, bool LDSBUF = false>
+__device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b, int s, int col, const uint32_t* in_bits, int mode,
+                                                uint32_t* scratch = nullptr) {
     const int l = lane_id();
     const int pw = c.nin_pad >> 5;
     const size_t ms = (size_t)model_stream(c, s);
     const uint32_t* prow = b.potmask + (ms * c.ncol + col) * pw;
-    float* perm = sp_perm_row<PAGED_OK>(c, b, s, col);
+    float* perm = sp_perm_row<PAGED_OK, LDSBUF>(c, b, s, col, scratch);
     if (!perm) return;
     uint32_t* connT = b.connT + ms * c.nin_pad * c.nw;
     const uint32_t cw = (uint32_t)col >> 5, cb = 1u << (col & 31);
@@ -730,7 +838,7 @@ __device__ __forceinline__ void sp_load_input(const DevCfg& c, const SpBufs& b, 
 // learning with boostStrength != 0); enc: RDSE engines' encoded lists of the step.
 // planes: LDS for the waves' partial overlaps (SP_PLANE_WORDS; SpShared input
 // only), or null for the one-wave overlap.
-template <bool LEARN, bool PAGED_OK = true, class SH, class IN>
+template <bool LEARN, bool PAGED_OK = true, bool PLANES = false, class SH, class IN>
 __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, const IN* input, int s,
                                              SH& sh, int write_overlaps, uint32_t* bkey = nullptr,
                                              const uint16_t* enc = nullptr, uint32_t* planes = nullptr) {
@@ -761,8 +869,14 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     }
 #endif
     if (!LEARN) return;  // (callers synchronise before reading b.act)
-    // ---- adaptSynapses_: one wave per active column
-    for (int a = wave_id(); a < nact; a += blockDim.x >> 6) sp_adapt_column<PAGED_OK>(c, b, s, sh.actlist[a], sh.in, 0);
+    // ---- adaptSynapses_: one wave per active column (a paged column's first
+    // change replays its initial values through the wave's share of the
+    // overlap planes, free now: 512 words per wave)
+    constexpr bool LB = PLANES && std::is_same<SH, SpShared>::value;  // (PLANES: the fused kernels' planes)
+    static_assert(!LB || (TM_NT / 64) * 512 <= SP_PLANE_WORDS, "replay scratch: 512 words per wave");
+    uint32_t* scratch = LB ? planes + wave_id() * 512u : nullptr;
+    for (int a = wave_id(); a < nact; a += blockDim.x >> 6)
+        sp_adapt_column<PAGED_OK, LB>(c, b, s, sh.actlist[a], sh.in, 0, scratch);
     __syncthreads();
     // ---- updateDutyCycles_ (period = min(dutyCyclePeriod, iterationNum))
     float* odc = b.duty + (size_t)model_stream(c, s) * 2 * c.ncol;
@@ -795,7 +909,8 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     const int nb = sh.nbump;
     if (nb > 0) {
         // ascending order is irrelevant: each column is updated independently
-        for (int k = wave_id(); k < nb; k += blockDim.x >> 6) sp_adapt_column<PAGED_OK>(c, b, s, sh.bump[k], sh.in, 1);
+        for (int k = wave_id(); k < nb; k += blockDim.x >> 6)
+            sp_adapt_column<PAGED_OK, LB>(c, b, s, sh.bump[k], sh.in, 1, scratch);
     }
     // ---- isUpdateRound_: updateMinDutyCyclesGlobal_
     if (sh.iter % (uint32_t)c.update_period == 0) {

@@ -120,7 +120,7 @@ enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
 // (SC_HIST .. SC_HIST + 8 are the histogram) learning counts: pool scans and
 // the slots they swept, SP paged-row replays and the lane-0 cycles they took
 // (summed over waves; filled in by htm_debug_stamps from SpBufs::dbg)
-enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC };
+enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC, SC_REPLAYSAMPLE, SC_REPLAYSKIP };
 
 // ---------------------------------------------------------------------------
 // LDS layout
@@ -2704,8 +2704,8 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_STAMPS
         if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (SPL && sp_learn) sp_step_body<true, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, bkey, enc, planes);
-        else sp_step_body<false, PAGED_OK>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
+        if (SPL && sp_learn) sp_step_body<true, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, bkey, enc, planes);
+        else sp_step_body<false, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
         __syncthreads();
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
                                     k == k1 - 1);
