@@ -711,7 +711,7 @@ static int flush_async(htm_engine* e, hipStream_t st) {
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
     if (e->flush_mode == 1 || st == e->fstream) {
         // on the stream of the steps, after them: the bound is fx_dn itself
-        if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1))
+        if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1, 0))
             return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
         e->defer_steps = 0;
         return HTM_OK;
@@ -719,7 +719,7 @@ static int flush_async(htm_engine* e, hipStream_t st) {
     if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
     HIP_TRY(hipEventRecord(e->ev_logged, st));
     HIP_TRY(hipStreamWaitEvent(e->fstream, e->ev_logged, 0));
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, e->fstream, 0))
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, e->flush_wg, e->fstream, 0, 0))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     HIP_TRY(hipEventRecord(e->ev_flushed, e->fstream));
     e->defer_steps = 0;
@@ -737,7 +737,8 @@ static int flush_deferred(htm_engine* e, hipStream_t st) {
         e->flush_pending = false;
     }
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1))
+    // (the caller waits on it: split per rank window, the latency of one window)
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1, 1))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     e->defer_steps = 0;
     return HTM_OK;

@@ -207,7 +207,8 @@ struct TmBufs {
     uint32_t* fx_fq;               // [FX_FLUSH_WG][q_cap] the flush workgroups' qualifying lists
     uint32_t* fx_fwork;            // [4] flush job counter, error flags (FX_ERR_*), jobs
     uint32_t* fx_fjobs;            // [S * fx_dcap * fx_nwin] the running flush's jobs:
-                                   //     (stream * fx_dcap + ring slot) * fx_nwin + rank window
+                                   //     (stream * fx_dcap + ring slot) * (fx_nwin + 1) + rank window
+                                   //     (fx_nwin: every window of the entry)
 };
 
 // deferred-log flush error flags (fx_fwork[1]; htm_status / htm_counters)
@@ -451,7 +452,7 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
                    uint32_t* wq, int unit_steps, hipStream_t st);
 int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n, hipStream_t st);
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
-int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn);
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn, int split);
 int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

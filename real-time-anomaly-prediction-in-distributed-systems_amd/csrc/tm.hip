@@ -349,13 +349,16 @@ int tm_configure_lds(const DevCfg& c) {
 // only to that flush's fx_dupto; a stale read leaves it fewer free slots,
 // never more).  Every job is checked before use (FX_ERR_JOB): a bad one is
 // skipped and flagged, never dereferenced.
-// A job is one rank window of one logged entry: the windows of a bursting set
-// (the longest jobs) run on separate workgroups, so a flush -- the one that
-// ends a timed region above all -- takes about one window's counting.
+// A job is one logged entry, or (split flushes) one rank window of it: split,
+// the windows of a bursting set (the longest jobs) run on separate workgroups,
+// so the flush takes about one window's counting -- what a flush that a
+// caller waits for wants (htm_flush, the end of a timed region); unsplit, the
+// per-job setup is paid once per entry -- what the periodic flushes want
+// (profiles/r04_ab/flush_split.txt).
 __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, int n) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t job;
-    const uint32_t dcap = (uint32_t)c.fx_dcap, nwin = (uint32_t)c.fx_nwin;
+    const uint32_t dcap = (uint32_t)c.fx_dcap, nwin = (uint32_t)c.fx_nwin, stride = nwin + 1u;
     const uint32_t cap = (uint32_t)n * dcap * nwin;
     uint32_t total = b.fx_fwork[2];  // the job list (tm_fx_jobs_kernel, the launch before)
     if (total > cap) {
@@ -368,9 +371,9 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
         __syncthreads();
         const uint32_t jj = __builtin_amdgcn_readfirstlane(job);
         if (jj >= total) break;
-        // (stream * dcap + ring slot) * nwin + window
+        // (stream * dcap + ring slot) * (nwin + 1) + window (nwin: every window)
         const uint32_t jw = __builtin_amdgcn_readfirstlane(b.fx_fjobs[jj]);
-        const uint32_t win = jw % nwin, j = jw / nwin;
+        const uint32_t win = jw % stride, j = jw / stride;
         const uint32_t su = j / dcap;
         const uint32_t i = j % dcap;
         const uint32_t len0 = su < (uint32_t)n ? (uint32_t)b.fx_dlen[(size_t)su * dcap + i] : 0xFFFFFFFFu;
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
             if (cell < (uint32_t)c.ncells) atomicOr(&t.infA[cell >> 5], 1u << (cell & 31));
         }
         __syncthreads();
-        collect_frozen(t, c.act_thr, FX_WIN, (int)win);
+        collect_frozen(t, c.act_thr, FX_WIN, win < nwin ? (int)win : -1);
         __syncthreads();
         if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)c.q_cap) {
             atomicOr(&b.fx_fwork[1], FX_ERR_QCAP);  // qualifying-list overflow, as in the step (htm_status)
@@ -423,7 +426,7 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
 // flushed without having been replayed.  One workgroup per stream.
 // from_dn: the flush runs on the step stream after the steps (nothing appends
 // meanwhile), so the bound is fx_dn itself -- no snapshot launch.
-__global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n, int from_dn) {
+__global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n, int from_dn, int split) {
     __shared__ uint32_t hsh[64], len[64], keep[64];
     const int s = blockIdx.x;
     const uint32_t dcap = (uint32_t)c.fx_dcap;
@@ -483,11 +486,13 @@ __global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        // one job per (kept entry, rank window of the stream's model)
+        // one job per kept entry, or per (kept entry, rank window of the
+        // stream's model) when split
         const uint32_t nwin = (uint32_t)c.fx_nwin, W = (uint32_t)c.fx_win;
         const uint32_t nr = b.fx_nr[model_stream(c, s)];
         uint32_t nw = (nr + W - 1u) / W;
         nw = nw < nwin ? nw : nwin;
+        if (!split) nw = 1u;
         uint32_t m = 0;
         for (uint32_t i = 0; i < p; i++) m += keep[i];
         uint32_t base = atomicAdd(&b.fx_fwork[2], m * nw);
@@ -496,7 +501,7 @@ __global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int
             if (!keep[i]) continue;
             const uint32_t e = (uint32_t)s * dcap + (f + i) % dcap;
             for (uint32_t w = 0; w < nw; w++, base++) {
-                if (base < cap) b.fx_fjobs[base] = e * nwin + w;
+                if (base < cap) b.fx_fjobs[base] = e * (nwin + 1u) + (split ? w : nwin);
                 else atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
             }
         }
@@ -525,14 +530,14 @@ int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn) {
+int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn, int split) {
     if (n <= 0 || !b.fx_dlog) return 0;
     const size_t lds = tm_step_lds_bytes(c, 0, 1);
-    const int total = n * c.fx_dcap * c.fx_nwin;
+    const int total = n * c.fx_dcap * (split ? c.fx_nwin : 1);
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
-    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3(n), dim3(256), 0, st, c, b, n, from_dn);
+    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3(n), dim3(256), 0, st, c, b, n, from_dn, split);
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;

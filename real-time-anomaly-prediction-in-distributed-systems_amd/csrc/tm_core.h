@@ -2289,6 +2289,14 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
 // the flag, and the next step starts from the dense copy).  Uses t.flags and
 // the head of t.U (free after the TM step).  Returns the bytes this thread
 // moved.  Contains barriers.
+// (A/B builds, -DHTM_WB_SC1: the write-back's stores as agent-scope relaxed
+// atomic stores -- global_store sc1, which leave the XCD L2 at once instead of
+// staying dirty for the end-of-kernel writeback)
+#ifdef HTM_WB_SC1
+#define WB_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define WB_ST(p, v) (*(p) = (v))
+#endif
 __device__ __forceinline__ uint32_t write_back_inference(Tm& t, uint32_t* gbm, float* gval, uint32_t* gnz) {
     const DevCfg& c = t.c;
     uint32_t* nzb = t.flags;  // the new bitmap
@@ -2307,8 +2315,8 @@ __device__ __forceinline__ uint32_t write_back_inference(Tm& t, uint32_t* gbm, f
     // pointers trip an LLVM gfx950 verifier error in the paged kernel)
     uint32_t wb = 0;
     for (int w = threadIdx.x; w < c.cw; w += TM_NT) {
-        gbm[w] = t.infA[w];
-        gbm[c.cw + w] = t.infP[w];
+        WB_ST(&gbm[w], t.infA[w]);
+        WB_ST(&gbm[c.cw + w], t.infP[w]);
         wb += 8;
     }
     __syncthreads();
@@ -2318,7 +2326,7 @@ __device__ __forceinline__ uint32_t write_back_inference(Tm& t, uint32_t* gbm, f
     const uint32_t off = wg_excl_scan(t.sh, mine, &tot);
     if (threadIdx.x < (uint32_t)c.nw) {
         woff[threadIdx.x] = off;
-        gnz[threadIdx.x] = nzb[threadIdx.x];
+        WB_ST(&gnz[threadIdx.x], nzb[threadIdx.x]);
         wb += 4;
     }
     if (threadIdx.x == 0) {
@@ -2329,7 +2337,7 @@ __device__ __forceinline__ uint32_t write_back_inference(Tm& t, uint32_t* gbm, f
     for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
         const uint32_t w = nzb[col >> 5];
         if ((w >> (col & 31)) & 1u) {
-            gval[woff[col >> 5] + __popc(w & ((1u << (col & 31)) - 1u))] = t.colconf[col];
+            WB_ST(&gval[woff[col >> 5] + __popc(w & ((1u << (col & 31)) - 1u))], t.colconf[col]);
             wb += 4;
         }
     }
