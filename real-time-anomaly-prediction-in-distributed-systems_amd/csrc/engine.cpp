@@ -105,6 +105,8 @@ struct htm_engine {
     int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
     bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
+    unsigned long long* wg_trace = nullptr;  // A/B builds: HTM_WG_TRACE timeline of the latest lockstep launch
+    size_t wg_trace_cap = 0;
 };
 
 
@@ -900,6 +902,18 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     } else {
         tb.fx_dlog = nullptr;
     }
+#ifdef HTM_AB_KNOBS
+    // A/B builds: every workgroup's start / end time of the latest lockstep launch
+    if (ab_knob("HTM_WG_TRACE") && n_steps == 1) {
+        if (!e->wg_trace) {
+            e->wg_trace_cap = (size_t)e->n;
+            HIP_TRY(hipMalloc(&e->wg_trace, e->wg_trace_cap * 64));
+            e->allocs.push_back(e->wg_trace);
+        }
+        HIP_TRY(hipMemsetAsync(e->wg_trace, 0, e->wg_trace_cap * 64, st));
+        tb.wg_trace = e->wg_trace;
+    }
+#endif
     if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
@@ -1494,6 +1508,20 @@ uint64_t htm_sp_perm_rows_used(htm_engine* e) {
         return 0;
     return std::min<unsigned long long>(x, e->dc.pool_rows);
 }
+
+#ifdef HTM_AB_KNOBS
+// A/B builds only (not in htm_amd.h): the HTM_WG_TRACE timeline of the latest
+// lockstep launch, [workgroup][8] (start, end, HW_ID, XCC_ID, step bytes, final
+// active cells); returns the rows copied.
+int64_t htm_ab_wg_trace(htm_engine* e, unsigned long long* out, int64_t max_rows) {
+    if (!e || !e->wg_trace || !out) return 0;
+    const int64_t rows = std::min<int64_t>(max_rows, (int64_t)e->wg_trace_cap);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, e->wg_trace, (size_t)rows * 64, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return rows;
+}
+#endif
 
 int32_t htm_frozen_index_valid(const htm_engine* e) { return e && e->fx_valid ? 1 : 0; }
 

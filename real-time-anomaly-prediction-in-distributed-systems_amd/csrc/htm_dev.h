@@ -209,6 +209,8 @@ struct TmBufs {
     uint32_t* fx_fjobs;            // [S * fx_dcap * fx_nwin] the running flush's jobs:
                                    //     (stream * fx_dcap + ring slot) * (fx_nwin + 1) + rank window
                                    //     (fx_nwin: every window of the entry)
+    unsigned long long* wg_trace;  // A/B builds (HTM_WG_TRACE): [grid][8] start / end (s_memrealtime),
+                                   //     HW_ID, XCC_ID, step bytes, final active cells; else null
 };
 
 // deferred-log flush error flags (fx_fwork[1]; htm_status / htm_counters)

@@ -2667,6 +2667,9 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
     // one unit per stream (n_steps <= unit_steps, e.g. every htm_step): no
     // hand-offs, so no queue and no fences -- workgroup b runs stream b
     const bool direct = nblk == 1;
+#ifdef HTM_AB_KNOBS
+    const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint32_t u = 0xFFFFFFFFu;
     int s = 0, k = 0, k0 = 0, k1 = 0;
     for (;;) {
@@ -2720,6 +2723,32 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
         __syncthreads();
         k++;
     }
+#ifdef HTM_AB_KNOBS
+    // A/B builds: the workgroup timeline of a lockstep launch (tools/wg_timeline.py)
+    if (b.wg_trace && direct) {
+        const uint32_t* infA = reinterpret_cast<const uint32_t*>(lds + tm_layout(c, LEARN, FROZEN).off_bm);
+        uint32_t pc = 0;
+        if (blockIdx.x < (uint32_t)n)
+            for (int i = threadIdx.x; i < c.cw; i += TM_NT) pc += __popc(infA[i]);
+        pc = wave_sum_u32(pc);
+        __syncthreads();
+        if (lane_id() == 0 && wave_id() < 3) unit_sh[wave_id()] = pc;
+        __syncthreads();
+        const uint32_t tot = unit_sh[0] + unit_sh[1] + unit_sh[2];
+        __syncthreads();
+        if (wave_id() == 3 && lane_id() == 0) unit_sh[0] = tot + pc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long* p = b.wg_trace + (size_t)blockIdx.x * 8;
+            p[0] = wg_t0;
+            p[1] = __builtin_amdgcn_s_memrealtime();
+            p[2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            p[3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+            p[4] = blockIdx.x < (uint32_t)n ? reinterpret_cast<TmSh*>(lds)->bytes : 0ull;
+            p[5] = unit_sh[0];
+        }
+    }
+#endif
 }
 
 #define HTM_RUN_ARGS                                                                                          \
