@@ -180,6 +180,11 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    beside the next steps, 1 on the step stream after them (full width).
                                    Results are identical; the default is chosen by measurement from the
                                    engine size (deferred dutyCycle() writes) */
+#define HTM_OPT_ORDERED 12      /* 1 (default): a frozen lockstep step (htm_step) of a dense-SP engine of
+                                   at most 16,384 streams runs the SP kernel, lists the streams by the
+                                   cost of their TM step (the active cells phase 1 will list), and runs
+                                   the TM steps heaviest first; results are identical.  0: one fused
+                                   SP+TM workgroup per stream in stream order */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued

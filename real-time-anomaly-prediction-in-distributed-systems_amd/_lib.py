@@ -47,6 +47,7 @@ OPT_RUN_CHUNK = 6
 OPT_RUN_UNIT = 7
 OPT_DEFER_DUTY = 10
 OPT_FLUSH_MODE = 11
+OPT_ORDERED = 12
 
 
 class HtmConfig(ctypes.Structure):

@@ -105,6 +105,9 @@ struct htm_engine {
     int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
     bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
+    int32_t ordered = 1;              // HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first
+    uint32_t* ord = nullptr;          // [n] the ordered launch's stream of each workgroup
+    uint16_t* ord_est = nullptr;      // [n] each stream's TM cost estimate (sp_step_ord_kernel)
     unsigned long long* wg_trace = nullptr;  // A/B builds: HTM_WG_TRACE timeline of the latest lockstep launch
     size_t wg_trace_cap = 0;
 };
@@ -512,6 +515,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (n_streams > 16384) e->flush_mode = 1;
     if (const char* env = ab_knob("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
+    if (const char* env = ab_knob("HTM_ORDERED")) e->ordered = std::atoi(env) ? 1 : 0;               // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (r && !ab_knob("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
@@ -648,6 +652,7 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         if (int r = flush_sync(e)) return r;
         e->flush_mode = value;
     }
+    else if (opt == HTM_OPT_ORDERED) e->ordered = value ? 1 : 0;
     else if (opt == HTM_OPT_RUN_UNIT) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
         e->run_unit = value;
@@ -879,13 +884,19 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
                      int frozen) {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     const bool prof = profiled_launch(e);
+    // ordered lockstep step (HTM_OPT_ORDERED; frozen, one step, dense SP, at
+    // most 16,384 streams): the SP kernel, the cost-ordered stream list, then
+    // the fused kernel's TM steps in that order
+    const bool ordered = frozen && n_steps == 1 && !e->tm_learn && e->ordered && !e->dc.sp_paged && e->n <= 16384;
     if (prof) {
         int r = next_events(e, ev, n_steps);
         if (r) return r;
         // one event before and one after the fused kernel (an event record is
-        // a few microseconds of the queue's time: no empty "SP" interval)
-        e->ev_fused.back() = 1;
-        HIP_TRY(hipEventRecord(ev[1], st));
+        // a few microseconds of the queue's time: no empty "SP" interval);
+        // ordered: SP kernel + ordering, then the TM steps
+        if (ordered) HIP_TRY(hipEventRecord(ev[0], st));
+        else e->ev_fused.back() = 1;
+        if (!ordered) HIP_TRY(hipEventRecord(ev[1], st));
     }
     // auto unit: a stream keeps its TM state in LDS for a unit's steps; longer
     // units save state round trips and queue handoffs, shorter ones balance
@@ -894,11 +905,27 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     const int32_t unit = e->run_unit > 0 ? e->run_unit : std::max(16, std::min(64, n_steps / 8));
     if (int r = encode_rdse(e, d_values, n_steps, st)) return r;
     TmBufs tb = e->tm;
+    if (ordered) {
+        if (!e->ord) {
+            ALLOC(e->ord, uint32_t, e->n);
+            ALLOC(e->ord_est, uint16_t, e->n);
+        }
+        if (launch_sp_step_ord(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, e->tm.bm, e->ord_est, st))
+            return htm_fail(HTM_E_HIP, "sp_step launch");
+        if (launch_ord_sort(e->dc, e->ord_est, e->ord, e->n, st)) return htm_fail(HTM_E_HIP, "ord_sort launch");
+        if (prof) HIP_TRY(hipEventRecord(ev[1], st));
+        tb.ord = e->ord;
+        tb.tm_only = 1;
+    }
     // deferred dutyCycle() writes: frozen lockstep launches (one step)
     const bool defer = frozen && n_steps == 1 && e->defer;
     if (defer) {
         if (int r = alloc_dlog(e)) return r;
+        const uint32_t* ord = tb.ord;
+        const int32_t tm_only = tb.tm_only;
         tb = e->tm;
+        tb.ord = ord;
+        tb.tm_only = tm_only;
     } else {
         tb.fx_dlog = nullptr;
     }

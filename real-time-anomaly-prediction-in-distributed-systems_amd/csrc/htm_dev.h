@@ -211,7 +211,16 @@ struct TmBufs {
                                    //     (fx_nwin: every window of the entry)
     unsigned long long* wg_trace;  // A/B builds (HTM_WG_TRACE): [grid][8] start / end (s_memrealtime),
                                    //     HW_ID, XCC_ID, step bytes, final active cells; else null
+    // Ordered lockstep launches (HTM_OPT_ORDERED): the SP kernel has run every
+    // stream's SP, ord_sort_kernel has listed the streams heaviest TM step
+    // first (the active cells phase 1 will list), and the fused kernel runs
+    // the TM steps only, workgroup b taking stream ord[b]: the hardware
+    // dispatches workgroups in order, so the launch's longest steps start first
+    // instead of wherever the stream order puts them.
+    const uint32_t* ord;           // [S] stream of each workgroup (null: workgroup b runs stream b)
+    int32_t tm_only;               // 1: the launch skips the SP (ordered launches)
 };
+#define ORD_NB 64                  // cost buckets of the ordering (active-cell estimate / (max_act_cells / 64))
 
 // deferred-log flush error flags (fx_fwork[1]; htm_status / htm_counters)
 #define FX_ERR_QCAP 16u   // a replayed phase 2 overflowed q_cap (as in the step: results invalid)
@@ -456,6 +465,9 @@ int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn, int split);
 int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st);
+int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st);
+int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
+                       const uint32_t* tm_bm, uint16_t* est, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen);

@@ -287,6 +287,46 @@ __global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const 
     sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps, LEARN ? bkey : nullptr, enc);
 }
 
+// The SP of an ordered lockstep step (HTM_OPT_ORDERED, dense SP): the fused
+// kernel's four-wave SP, then the stream's TM cost estimate -- the active cells
+// TM phase 1 will list: a predicted column's predicted cells in
+// infPredictedState(t-1) (tm_bm), all K cells of a bursting one -- to est[s]
+// for ord_sort_kernel.
+template <bool LEARN>
+__global__ __launch_bounds__(256) void sp_step_ord_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps,
+                                                          const uint16_t* enc, const uint32_t* tm_bm, uint16_t* est) {
+    __shared__ SpShared sh;
+    __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
+    __shared__ uint32_t planes[SP_PLANE_WORDS];
+    const int s = blockIdx.x;
+    sp_step_body<LEARN, false, true>(c, b, values, s, sh, write_overlaps, LEARN ? bkey : nullptr, enc, planes);
+    __syncthreads();
+    if (wave_id() == 0) {
+        const int K = c.K, a = lane_id();
+        const int nact = sh.nact < HTM_MAXACT ? sh.nact : HTM_MAXACT;
+        const uint32_t* gp = tm_bm + (size_t)s * 4 * c.cw + c.cw;
+        uint32_t v = 0;
+        if (a < nact) {
+            const uint32_t f = bm_field(gp, (uint32_t)sh.actlist[a] * (uint32_t)K, (uint32_t)K);
+            v = f ? (uint32_t)__popc(f) : (uint32_t)K;
+        }
+        v = wave_sum_u32(v);
+        if (a == 0) est[s] = (uint16_t)(v < 65535u ? v : 65535u);
+    }
+}
+
+int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
+                       const uint32_t* tm_bm, uint16_t* est, hipStream_t st) {
+    const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? b.enc_in : nullptr;  // (one step: row 0)
+    if (learn)
+        hipLaunchKernelGGL(sp_step_ord_kernel<true>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps, enc,
+                           tm_bm, est);
+    else
+        hipLaunchKernelGGL(sp_step_ord_kernel<false>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps, enc,
+                           tm_bm, est);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Level-2 SP of Models 2/3 (SPRegion fed an SDR, MultiLevelNetworkModel.py:92-95):
 // the input bitmap is staged in LDS; one workgroup per stream.
 template <bool LEARN>

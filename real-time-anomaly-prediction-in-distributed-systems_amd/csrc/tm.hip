@@ -413,6 +413,42 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
     }
 }
 
+// Ordered lockstep launches (TmBufs::ord): after the SP kernel
+// (sp_step_ord_kernel: est[s], the active cells TM phase 1 will list -- what a
+// step's cost follows, profiles/r04_ab/lpt_sim.txt), list the streams heaviest
+// first: a counting sort over ORD_NB cost buckets by one workgroup (streams
+// within a bucket in no particular order -- streams are independent, so the
+// order never changes a result).
+__global__ __launch_bounds__(1024) void ord_sort_kernel(DevCfg c, const uint16_t* est, uint32_t* ord, int n) {
+    __shared__ uint32_t hist[ORD_NB], at[ORD_NB];
+    extern __shared__ uint8_t bkt[];  // [n] bucket of each stream
+    const uint32_t mac = (uint32_t)c.max_act_cells;
+    for (int q = threadIdx.x; q < ORD_NB; q += blockDim.x) hist[q] = 0;
+    __syncthreads();
+    for (int s = threadIdx.x; s < n; s += blockDim.x) {
+        uint32_t q = (uint32_t)(((unsigned long long)est[s] * ORD_NB) / (mac + 1u));
+        q = q < ORD_NB ? q : ORD_NB - 1;
+        bkt[s] = (uint8_t)q;
+        atomicAdd(&hist[q], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int q = ORD_NB - 1; q >= 0; q--) {  // heaviest bucket first
+            at[q] = run;
+            run += hist[q];
+        }
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < n; s += blockDim.x) ord[atomicAdd(&at[bkt[s]], 1u)] = (uint32_t)s;
+}
+
+int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st) {
+    if (n <= 0 || n > 65536) return -1;
+    hipLaunchKernelGGL(ord_sort_kernel, dim3(1), dim3(1024), (size_t)n, st, c, est, ord, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Before a flush (on the flush's stream): the entries [fx_dflushed, fx_dsnap)
 // of every stream as a compact job list, without repeats -- an entry whose
 // active set equals an earlier entry of the same batch (order-independent

@@ -2676,7 +2676,8 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
         if (k == k1 && direct) {
             if (u != 0xFFFFFFFFu || blockIdx.x >= (uint32_t)n) break;
             u = blockIdx.x;
-            s = (int)blockIdx.x;
+            s = b.ord ? (int)__builtin_amdgcn_readfirstlane(b.ord[blockIdx.x]) : (int)blockIdx.x;
+            if (s >= n) break;  // (never: ord is a permutation of the streams)
             k0 = k = 0;
             k1 = n_steps;
         }
@@ -2715,9 +2716,11 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_STAMPS
         if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (SPL && sp_learn) sp_step_body<true, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, bkey, enc, planes);
-        else sp_step_body<false, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
-        __syncthreads();
+        if (!b.tm_only) {
+            if (SPL && sp_learn) sp_step_body<true, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, bkey, enc, planes);
+            else sp_step_body<false, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
+            __syncthreads();
+        }
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
                                     k == k1 - 1);
         __syncthreads();

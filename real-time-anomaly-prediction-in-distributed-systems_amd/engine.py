@@ -241,6 +241,11 @@ class HTMEngine:
         engine's own HIP stream, 1 on the step stream (results identical)."""
         check(self._L.htm_set_option(self.h, _lib.OPT_FLUSH_MODE, int(mode)))
 
+    def ordered_steps(self, on: bool):
+        """Frozen lockstep steps run their TM steps heaviest first
+        (HTM_OPT_ORDERED, default on); results are identical either way."""
+        check(self._L.htm_set_option(self.h, _lib.OPT_ORDERED, int(on)))
+
     def sp_perm_rows_used(self) -> int:
         """Paged SP permanences: pool rows handed out (0 for a dense engine)."""
         return int(self._L.htm_sp_perm_rows_used(self.h))

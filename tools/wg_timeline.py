@@ -59,6 +59,10 @@ for k in range(64, 80):
     first_end = en[own].min()
     r["second_wave_owners"] = int((st[own] > first_end).sum())
     r["second_wave_dur_mean"] = float((en - st)[own][st[own] > first_end].mean()) if r["second_wave_owners"] else 0.0
+    r["ordered_sp_tm_jobs"] = [int((b[:, 6] >> 32).sum()), int((b[:, 6] & 0xFFFFFFFF).sum())]
+    tt = b[:, 7]
+    r["ordered_us_pick_sp_tm"] = [float(((tt >> 42) & 0x1FFFFF).sum() / 100.0), float(((tt >> 21) & 0x1FFFFF).sum() / 100.0),
+                                  float((tt & 0x1FFFFF).sum() / 100.0)]
     xcc = b[:, 3] & 0xF
     r["owners_per_xcc"] = np.bincount(xcc[own], minlength=8).tolist()
     res.append(r)
