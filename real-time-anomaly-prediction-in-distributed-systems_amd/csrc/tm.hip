@@ -432,12 +432,10 @@ __global__ __launch_bounds__(1024) void ord_sort_kernel(DevCfg c, const uint16_t
         atomicAdd(&hist[q], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int q = ORD_NB - 1; q >= 0; q--) {  // heaviest bucket first
-            at[q] = run;
-            run += hist[q];
-        }
+    static_assert(ORD_NB == 64, "one lane per bucket");
+    if (threadIdx.x < 64) {  // exclusive prefix, heaviest bucket first (lane l: bucket 63 - l)
+        const uint32_t h = hist[63 - threadIdx.x];
+        at[63 - threadIdx.x] = wave_incl_scan(h) - h;
     }
     __syncthreads();
     for (int s = threadIdx.x; s < n; s += blockDim.x) ord[atomicAdd(&at[bkt[s]], 1u)] = (uint32_t)s;
