@@ -444,6 +444,9 @@ def main():
     ap.add_argument("--flush-mode", choices=["auto", "0", "1"], default="auto",
                     help="where the deferred-write flush runs (HTM_OPT_FLUSH_MODE): 0 beside the steps on the "
                          "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
+    ap.add_argument("--ordered", choices=["on", "off"], default="on",
+                    help="HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first (on, the engine "
+                         "default) or one fused SP+TM workgroup per stream in stream order (off); results identical")
     ap.add_argument("--shape", choices=["model1", "yaml"], default="model1",
                     help="model1 (default): the reference's Model-1 parameters (12 cells/column); yaml: the "
                          "reference's model.yaml set (RDSE, boostStrength 3, 32 cells/column; configs 2 and 4)")
@@ -553,6 +556,8 @@ def main():
         eng.flush_mode(int(args.flush_mode))
     if args.run_unit:
         eng.set_run_unit(args.run_unit)
+    if args.ordered == "off" and not standin:
+        eng.ordered_steps(False)
     C = args.condition
     T = C + args.warmup + args.steps + args.other_steps
     if c4:
@@ -667,10 +672,12 @@ def main():
                                 "per-stream TM state, learn off" % shape_name if c4 else
                                 "config2: %s streams, SP+TM learn off, from the GPU-trained state" % shape_name),
                    "shape": args.shape,
-                   "mode": ("lockstep: one htm_step (one fused launch) per step, every stream advances one "
-                            "network.run(1) per step" if args.mode == "step" else
+                   "mode": ("lockstep: one htm_step per step, every stream advances one network.run(1) per step"
+                            + (" (ordered: SP kernel, cost-ordered stream list, TM steps heaviest first)"
+                               if args.ordered == "on" and S <= 16384 and not c3 else "")
+                            if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
-                   "conditioning_steps": C, "flush_mode": args.flush_mode,
+                   "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
                    "cells_per_column": eng.cells_per_column,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
@@ -730,6 +737,8 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
                  "--no-learn-on", "--shape", args.shape]
         if args.flush_mode != "auto":
             child += ["--flush-mode", args.flush_mode]
+        if args.ordered != "on":
+            child += ["--ordered", args.ordered]
         for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows", "condition"):
             v = getattr(args, k)
             if v is not None:
