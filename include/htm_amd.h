@@ -185,6 +185,10 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    cost of their TM step (the active cells phase 1 will list), and runs
                                    the TM steps heaviest first; results are identical.  0: one fused
                                    SP+TM workgroup per stream in stream order */
+#define HTM_OPT_FLUSH_EVERY 13  /* lockstep steps between the periodic flushes of the deferred dutyCycle()
+                                   writes (0: the default, 8, at most half the log ring); a cadence past
+                                   the ring makes the log fill, and a full log makes a step count its
+                                   discarded phase 2s in full (results identical) */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued

@@ -48,6 +48,7 @@ OPT_RUN_UNIT = 7
 OPT_DEFER_DUTY = 10
 OPT_FLUSH_MODE = 11
 OPT_ORDERED = 12
+OPT_FLUSH_EVERY = 13
 
 
 class HtmConfig(ctypes.Structure):

@@ -653,6 +653,11 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         e->flush_mode = value;
     }
     else if (opt == HTM_OPT_ORDERED) e->ordered = value ? 1 : 0;
+    else if (opt == HTM_OPT_FLUSH_EVERY) {
+        if (value < 0) return htm_fail(HTM_E_INVALID, "flush cadence: 0 (default) or N >= 1 lockstep steps");
+        if (int r = flush_sync(e)) return r;
+        e->flush_every = value;
+    }
     else if (opt == HTM_OPT_RUN_UNIT) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "run unit must be >= 0 (0: auto)");
         e->run_unit = value;
@@ -946,7 +951,8 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
     e->conf_packed = true;
     if (prof) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
-    if (defer && ++e->defer_steps >= std::min(e->flush_every ? e->flush_every : FLUSH_EVERY, e->dc.fx_dcap / 2)) {
+    // (an explicit cadence, HTM_OPT_FLUSH_EVERY, is taken as given: past the ring the log fills)
+    if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : std::min(FLUSH_EVERY, e->dc.fx_dcap / 2))) {
         int r = flush_async(e, st);  // beside the next steps
         if (r) return r;
     }

@@ -241,6 +241,11 @@ class HTMEngine:
         engine's own HIP stream, 1 on the step stream (results identical)."""
         check(self._L.htm_set_option(self.h, _lib.OPT_FLUSH_MODE, int(mode)))
 
+    def flush_every(self, steps: int):
+        """Lockstep steps between periodic flushes of the deferred dutyCycle()
+        writes (HTM_OPT_FLUSH_EVERY; 0 = default)."""
+        check(self._L.htm_set_option(self.h, _lib.OPT_FLUSH_EVERY, int(steps)))
+
     def ordered_steps(self, on: bool):
         """Frozen lockstep steps run their TM steps heaviest first
         (HTM_OPT_ORDERED, default on); results are identical either way."""

@@ -29,17 +29,10 @@ def model1(rt, traces):
     return eng
 
 
-def replicas(rt, model1, n, env=None):
-    old = {k: os.environ.get(k) for k in (env or {})}
-    os.environ.update(env or {})
-    try:
-        e = rt.HTMEngine(n, seg_capacity=72 * 1024)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+def replicas(rt, model1, n, flush_every=0):
+    e = rt.HTMEngine(n, seg_capacity=72 * 1024)
+    if flush_every:
+        e.flush_every(flush_every)  # (HTM_OPT_FLUSH_EVERY: past the log ring, the log fills)
     for region in rt._lib.ST:
         e.import_state(region, model1.export_state(region, 0, 1), s0=0)
     e.replicate(0)
@@ -51,8 +44,8 @@ def lockstep(e, vals):
 
 
 @pytest.mark.parametrize("sp_learn", [False, True])
-@pytest.mark.parametrize("env", [{}, {"HTM_DEFER_FLUSH_EVERY": "100000"}], ids=["cadence", "log_fills"])
-def test_deferred_equals_undeferred(rt, model1, traces, sp_learn, env):
+@pytest.mark.parametrize("flush_every", [0, 100000], ids=["cadence", "log_fills"])
+def test_deferred_equals_undeferred(rt, model1, traces, sp_learn, flush_every):
     n, T = 96, 160
     rng = np.random.default_rng(17)
     test = np.asarray(traces["test"], np.float64)
@@ -60,7 +53,7 @@ def test_deferred_equals_undeferred(rt, model1, traces, sp_learn, env):
     s = np.arange(n)[None, :]
     vals = torch.tensor(np.clip(test[(t + 53 * s) % len(test)] + rng.integers(-2, 3, size=(T, n)), 0, 100),
                         device="cuda")
-    a = replicas(rt, model1, n, env)
+    a = replicas(rt, model1, n, flush_every)
     b = replicas(rt, model1, n)
     b.defer_duty(False)
     for e in (a, b):
