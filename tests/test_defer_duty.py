@@ -118,3 +118,32 @@ def test_frozen_learn_frozen_cycle(rt, model1, traces):
     for key in ("inf_phase2", "inf_backtracks", "lrn_phase2", "seg_live", "error"):
         assert ca[key] == cb[key], key
     assert ca["inf_backtracks"] > 0
+
+
+def test_flush_overlapping_snapshots(rt, model1, traces):
+    """A flush beside the steps (HTM_OPT_FLUSH_MODE 0) enqueued after every
+    step (HTM_OPT_FLUSH_EVERY 1) with 2,048 streams: each flush takes longer
+    than a step, so later snapshots land while earlier flushes run -- the
+    case the per-flush bound (fx_dupto) exists for.  Scores, counters and the
+    segment records (dutyCycle cache included) equal the undeferred engine."""
+    n, T = 2048, 48
+    rng = np.random.default_rng(43)
+    test = np.asarray(traces["test"], np.float64)
+    t = np.arange(T)[:, None]
+    s = np.arange(n)[None, :]
+    vals = torch.tensor(np.clip(test[(t + 37 * s) % len(test)] + rng.integers(-2, 3, size=(T, n)), 0, 100),
+                        device="cuda")
+    a = replicas(rt, model1, n, flush_every=1)
+    a.flush_mode(0)
+    b = replicas(rt, model1, n)
+    b.defer_duty(False)
+    for e in (a, b):
+        e.set_learning(False, False)
+    ga, gb = lockstep(a, vals), lockstep(b, vals)
+    assert np.array_equal(ga, gb)
+    ca, cb = a.counters(), b.counters()
+    for k in ("inf_phase2", "inf_backtracks", "seg_live", "error"):
+        assert ca[k] == cb[k], k
+    assert ca["error"] == 0 and ca["inf_backtracks"] > 0
+    for region in ("tm_seg_duty", "tm_seg_meta"):
+        assert np.array_equal(a.export_state(region), b.export_state(region)), region
