@@ -57,9 +57,13 @@ struct Region {
 // step's workgroups need (measured on config 2, 256-step regions ending with
 // htm_flush, profiles/r03_flush: 1,024 workgroups every 8 steps 0.319 ms per
 // step, 128 / 16 0.244, 256 / 8 0.243, the round-2 full-width flush on the
-// step stream every 32 steps 0.246; 20-step regions 0.278 / 0.258 / 0.269)
+// step stream every 32 steps 0.246; 20-step regions 0.278 / 0.258 / 0.269).
+// With ordered lockstep steps the TM launch's tail leaves more of the chip idle
+// and a wider flush fills it: 768 workgroups 0.1763 ms per step vs 256 0.1801
+// (512: 0.1764; 128-step regions), 20-step regions 0.1887 vs 0.1903
+// (profiles/r04_ab/flush_wg.txt)
 #define FLUSH_EVERY 8
-#define FLUSH_WG 256
+#define FLUSH_WG 768
 
 struct htm_engine {
     htm_config cfg;
