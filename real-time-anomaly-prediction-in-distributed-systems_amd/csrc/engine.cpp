@@ -902,9 +902,8 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         if (r) return r;
         // one event before and one after the fused kernel (an event record is
         // a few microseconds of the queue's time: no empty "SP" interval);
-        // ordered: SP kernel + ordering, then the TM steps
-        if (ordered) HIP_TRY(hipEventRecord(ev[0], st));
-        else e->ev_fused.back() = 1;
+        // ordered: around the TM launch only (its SP kernel and sort untimed)
+        e->ev_fused.back() = 1;
         if (!ordered) HIP_TRY(hipEventRecord(ev[1], st));
     }
     // auto unit: a stream keeps its TM state in LDS for a unit's steps; longer
@@ -922,7 +921,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         if (launch_sp_step_ord(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, e->tm.bm, e->ord_est, st))
             return htm_fail(HTM_E_HIP, "sp_step launch");
         if (launch_ord_sort(e->dc, e->ord_est, e->ord, e->n, st)) return htm_fail(HTM_E_HIP, "ord_sort launch");
-        if (prof) HIP_TRY(hipEventRecord(ev[1], st));
+        if (prof) HIP_TRY(hipEventRecord(ev[1], st));  // (the TM launch's start)
         tb.ord = e->ord;
         tb.tm_only = 1;
     }
