@@ -177,6 +177,7 @@ def bench_learn_on(args, rt, trace, world, rank, local, pmc_summary=None, pmc_no
     torch.cuda.synchronize()
     init_s = time.time() - t0
     eng.set_learning(True, True)
+    eng.split_learning(args.split_learn == "on")
     W, K = args.learn_warmup, args.learn_steps
     vals = torch.tensor(make_inputs(n_total, s0, s1, 0, W + K, trace), device=dev)
     scores = torch.empty((W + K, S), dtype=torch.float32, device=dev)
@@ -185,7 +186,12 @@ def bench_learn_on(args, rt, trace, world, rank, local, pmc_summary=None, pmc_no
     torch.cuda.synchronize()
     c0 = eng.counters()
     eng.profile(True)
-    dt, _ = timed_replay(eng, vals, scores, W, K, "step", 1, None, None, rank, world, dev)
+    marks = []
+    dt, _ = timed_replay(eng, vals, scores, W, K, "step", 1, None, None, rank, world, dev, marks=marks)
+    # the step time per 64-step window of the region (segment pools grow, fewer
+    # SP columns are new): HIP events on the step stream between the windows
+    per64 = [{"steps": f"{W + k0}-{W + k1 - 1}", "ms_per_step": round(e0.elapsed_time(e1) / (k1 - k0), 4)}
+             for (k0, e0), (k1, e1) in zip(marks, marks[1:])]
     prof = eng.profile_read()
     eng.profile(False)
     c1 = eng.counters()
@@ -194,17 +200,20 @@ def bench_learn_on(args, rt, trace, world, rank, local, pmc_summary=None, pmc_no
     seg_live = (c0["seg_live"] + c1["seg_live"]) / 2
     per_ss = learn_on_bytes(eng, S, seg_live)
     launches = prof["launches"]
-    avg_ms = prof["tm_ms"] / launches
+    split = args.split_learn == "on"
+    tm_name = kernel_name(True, False, True, split)
+    # a split step's kernels: the SP kernel (its learning) and the TM-only kernel, timed each
+    avg_ms = (prof["tm_ms"] + prof["sp_ms"]) / launches
     per_launch = per_ss * S
     achieved = per_launch / (avg_ms * 1e-3) / 1e9
-    traffic, tsrc = None, pmc_note
+    traffic, tsrc, k = None, pmc_note, None
     if pmc_summary:
-        k = pmc_kernel(pmc_summary, "htm_run_kernel<true>")
-        if k:
-            traffic = int(k["hbm_bytes_per_dispatch"])
-            tsrc = f"rocprofv3 --pmc passes of the learn-on leg ({pmc_summary}): {k.get('formula', '')}"
+        traffic, k = split_traffic(pmc_summary, split, tm_name)
+        if traffic:
+            tsrc = (f"rocprofv3 --pmc passes of the learn-on leg ({pmc_summary}): {k.get('formula', '')}"
+                    + (f", {tm_name} + {SP_LEARN_KERNEL}" if split else ""))
     rec = {"value": round(n_total * K / dt, 1), "unit": "stream-steps/s", "steps": K, "warmup": W,
-           "ms_per_step": round(dt / K * 1e3, 4),
+           "ms_per_step": round(dt / K * 1e3, 4), "per_64_steps": per64,
            "config": {"workload": "config3: fresh Model-1 streams (seed 2045+s), SP+TM learning on, lockstep htm_step",
                       "streams_per_gpu": S, "total_streams": n_total, "sp_perm_rows": 800,
                       "sp_perm_rows_used_per_stream": round(eng.sp_perm_rows_used() / S, 1),
@@ -213,12 +222,68 @@ def bench_learn_on(args, rt, trace, world, rank, local, pmc_summary=None, pmc_no
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                         "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
-                        "traffic_source": tsrc, "kernel": "htm_run_kernel<true>", "avg_launch_ms": round(avg_ms, 4),
+                        "traffic_source": tsrc,
+                        "kernel": f"{SP_LEARN_KERNEL} + {tm_name}" if split else tm_name,
+                        "avg_launch_ms": round(avg_ms, 4), "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4),
+                        "tm_kernel_avg_ms": round(prof["tm_ms"] / launches, 4),
                         "bytes_per_launch": int(per_launch), "bytes_per_stream_step": int(per_ss),
-                        "bytes_rule": "unique bytes (bench.learn_on_bytes, SURVEY.md 8(d) learning terms)"},
+                        "bytes_rule": "unique bytes (bench.learn_on_bytes, SURVEY.md 8(d) learning terms)",
+                        "issue": issue_record(k)},
            "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks", "lrn_phase2", "lrn_backtracks"]}}
     eng.close()
     return rec
+
+
+def sp_learn_bytes(eng):
+    """Algorithmic bytes per stream-step of an SP learning step beyond its
+    inference (SURVEY.md 8(d)'s SP learning terms, each byte once): the
+    winners' potential permanences read and written and their potential-mask
+    rows, both duty-cycle arrays read and written."""
+    c = eng.config
+    pw = (c.n_fields * c.enc_n + 31) // 32
+    n_pot = int(round(c.n_fields * c.enc_n * c.sp_potential_pct))
+    return c.sp_num_active * (n_pot * 4 * 2 + pw * 4) + 2 * c.sp_columns * 4 * 2
+
+
+def bench_test_phase(args, eng, vals, scores, a, n_total, S, rank, world, dev):
+    """The reference's test phase: ModelTesting.py:66 -> NetworkModel.py:40-44
+    leave SP learning ON and switch TM learning OFF, so a test record runs the
+    SP's adaptSynapses / duty cycles and the frozen TM.  The config-2 engine
+    (1,024 replicas of the GPU-trained state, after the headline regions),
+    `test_phase_warmup` untimed + `test_phase_steps` timed lockstep steps, the
+    barrier / max-over-ranks contract.  A lockstep step of this mode runs the
+    SP kernel (with learning) and then the TM-only frozen launch
+    (htm_run_frozen_kernel, ordered); its roofline is the whole step's
+    algorithmic bytes -- the TM kernel's own count plus the SP learning terms
+    (sp_learn_bytes) -- over the wall-clock step time (both kernels and the sort
+    inside it), a lower bound on the bandwidth the step achieves."""
+    W, K = args.test_phase_warmup, args.test_phase_steps
+    eng.set_learning(True, False)
+    for k in range(a, a + W):
+        eng.step(vals[k], out=scores[k])
+    import torch
+    torch.cuda.synchronize()
+    c0 = eng.counters()
+    dt, _ = timed_replay(eng, vals, scores, a + W, K, "step", 1, None, None, rank, world, dev)
+    c1 = eng.counters()
+    if c1["error"]:
+        raise RuntimeError(f"test-phase engine overflow flags {c1['error']}")
+    tm_per_ss = (c1["tm_bytes"] - c0["tm_bytes"]) / (K * S)
+    per_ss = tm_per_ss + sp_learn_bytes(eng)
+    achieved = per_ss * S / (dt / K) / 1e9
+    eng.set_learning(False, False)
+    return {"value": round(n_total * K / dt, 1), "unit": "stream-steps/s", "steps": K, "warmup": W,
+            "ms_per_step": round(dt / K * 1e3, 4),
+            "config": {"workload": "config2 streams (GPU-trained Model-1 replicas), SP learning ON, TM learning OFF: "
+                                   "the reference's test phase (ModelTesting.py:66, NetworkModel.py:40-44), lockstep",
+                       "mode": "lockstep: SP kernel with learning, cost-ordered stream list, TM-only frozen launch",
+                       "streams_per_gpu": S, "total_streams": n_total},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_stream_step": int(per_ss),
+                         "tm_bytes_per_stream_step": int(tm_per_ss), "sp_learn_bytes_per_stream_step": sp_learn_bytes(eng),
+                         "time_basis": "wall-clock ms_per_step (SP kernel + sort + TM launch + flushes)",
+                         "kernels": "sp_step_ord_kernel<true>, ord_sort_kernel, htm_run_frozen_kernel"},
+            "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]}}
 
 
 def launch_ranks(n):
@@ -253,7 +318,7 @@ def bench_build_info(rt):
 def pmc_kernel(path, base):
     pm = json.load(open(path))
     ks = [v for n, v in pm.get("kernels", {}).items()
-          if n.split("(")[0].replace("void ", "").strip() == base and "hbm_bytes_per_dispatch" in v]
+          if n.split("(")[0].replace("void ", "").strip() == base and ("hbm_bytes_per_dispatch" in v or "sq" in v)]
     return ks[0] if ks else None
 
 
@@ -438,15 +503,25 @@ def main():
     ap.add_argument("--no-learn-on", action="store_true",
                     help="config 2: skip the learn_on sub-record (config 3's learning streams, BASELINE's 'learn on')")
     ap.add_argument("--learn-streams", type=int, default=65536, help="learn_on: streams per GPU")
-    ap.add_argument("--learn-steps", type=int, default=32, help="learn_on: timed lockstep steps")
-    ap.add_argument("--learn-warmup", type=int, default=8, help="learn_on: untimed steps")
+    ap.add_argument("--learn-steps", type=int, default=240,
+                    help="learn_on: timed lockstep steps (SURVEY.md 8(d) config 3: T = 256 = 16 untimed + 240)")
+    ap.add_argument("--learn-warmup", type=int, default=16, help="learn_on: untimed steps")
     ap.add_argument("--pmc-summary-learn", default=None, help="counter summary of the learn_on leg (see --pmc-summary)")
+    ap.add_argument("--no-test-phase", action="store_true",
+                    help="config 2: skip the test_phase sub-record (SP learning on, TM learning off: the "
+                         "reference's test phase, NetworkModel.py:40-44)")
+    ap.add_argument("--test-phase-steps", type=int, default=256, help="test_phase: timed lockstep steps")
+    ap.add_argument("--test-phase-warmup", type=int, default=16, help="test_phase: untimed steps")
     ap.add_argument("--flush-mode", choices=["auto", "0", "1"], default="auto",
                     help="where the deferred-write flush runs (HTM_OPT_FLUSH_MODE): 0 beside the steps on the "
                          "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
     ap.add_argument("--ordered", choices=["on", "off"], default="on",
                     help="HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first (on, the engine "
                          "default) or one fused SP+TM workgroup per stream in stream order (off); results identical")
+    ap.add_argument("--split-learn", choices=["on", "off"], default="on",
+                    help="HTM_OPT_SPLIT_LEARN (config 3 and the learn_on leg): learning lockstep steps run the SP "
+                         "kernel then the TM-only learning kernel (on, the engine default) or one fused kernel (off); "
+                         "results identical")
     ap.add_argument("--shape", choices=["model1", "yaml"], default="model1",
                     help="model1 (default): the reference's Model-1 parameters (12 cells/column); yaml: the "
                          "reference's model.yaml set (RDSE, boostStrength 3, 32 cells/column; configs 2 and 4)")
@@ -540,6 +615,7 @@ def main():
         sync()
         train_s, hdr, model_dist = time.time() - t0, None, "fresh per-stream init"
         eng.set_learning(True, True)
+        eng.split_learning(args.split_learn == "on")
     elif c4:
         # one model trained on the GPU (2184 Model-1 records), shared by every stream
         model, train_s, hdr, model_dist = trained_engine(rt, 1, args.seg_capacity, local, train_vals, world=world,
@@ -559,7 +635,12 @@ def main():
     if args.ordered == "off" and not standin:
         eng.ordered_steps(False)
     C = args.condition
-    T = C + args.warmup + args.steps + args.other_steps
+    # the reference's test phase (SP learning on, TM learning off) on the same
+    # engine after the headline and run-mode regions: config 2, Model-1 shape
+    test_phase = (args.config == 2 and args.shape == "model1" and not args.no_test_phase and not standin
+                  and args.test_phase_steps > 0)
+    TP0 = C + args.warmup + args.steps + args.other_steps
+    T = TP0 + ((args.test_phase_warmup + args.test_phase_steps) if test_phase else 0)
     if c4:
         # per-rank jitter stream (a 1M x T matrix per rank would not fit host memory)
         rng = np.random.Generator(np.random.PCG64([724, s0]))
@@ -611,13 +692,19 @@ def main():
                              rank, world, dev)
         other = {"mode": omode, "value": round(n_total * args.other_steps / dl, 1), "steps": args.other_steps,
                  "ms_per_step": round(dl / args.other_steps * 1e3, 4)}
+    tp_rec = bench_test_phase(args, eng, vals, scores, TP0, n_total, S, rank, world, dev) if test_phase else None
     shape_name = ("model.yaml-shape (RDSE resolution 0.88, SP boostStrength 3.0, 2048 columns, 32-cell "
                   "BacktrackingTM; ML/HTM/params/model.yaml)" if args.shape == "yaml" else
                   "Model-1 (2048-col SP, 12-cell BacktrackingTM)")
+    # the engine's ordered lockstep path (HTM_OPT_ORDERED): frozen, one step per
+    # launch, dense SP permanences, at most 16,384 streams per GPU
+    ordered = (args.ordered == "on" and args.mode == "step" and S <= 16384 and not c3 and not args.sp_perm_rows
+               and not standin)
     roof = None
+    split = c3 and args.split_learn == "on" and args.mode == "step" and not standin
     if prof is not None and prof["tm_ms"] > 0:
         launches = prof["launches"]
-        avg_ms = prof["tm_ms"] / launches
+        avg_ms = (prof["tm_ms"] + (prof["sp_ms"] if split else 0.0)) / launches
         if c3:  # learning: unique bytes (the in-kernel count charges every pool re-scan)
             per_launch = learn_on_bytes(eng, S, (c0["seg_live"] + c1["seg_live"]) / 2) * S * prof["steps"] / launches
         else:   # frozen inference: the kernel's own count of the index blocks and state it moves,
@@ -629,18 +716,23 @@ def main():
         if args.pmc_summary:
             # HBM bytes per launch measured by rocprofv3 --pmc passes of THIS command
             # (tools/pmc_summary.py, run in the same gpurun call; corrections there)
-            k = pmc_kernel(args.pmc_summary, kernel_name(c3, c4, eng.fused))
-            if k:
-                traffic = int(k["hbm_bytes_per_dispatch"])
+            traffic, k = split_traffic(args.pmc_summary, split, kernel_name(c3, c4, eng.fused, split))
+            if traffic:
                 tsrc = (f"rocprofv3 --pmc passes of this command ({args.pmc_summary}): {k.get('formula', '')}; "
                         "calibrated on tools/fetch_calib (profiles/r02_final/pmc_summary.json)")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
-                "traffic_source": tsrc, "kernel": kernel_name(c3, c4, eng.fused),
+                "traffic_source": tsrc,
+                "kernel": (f"{SP_LEARN_KERNEL} + " if split else "") + kernel_name(c3, c4, eng.fused, split),
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
-                "profiled_launches": launches, "bytes_per_launch": int(per_launch),
-                "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
+                "profiled_launches": launches, "bytes_per_launch": int(per_launch), "issue": issue_record(k),
+                "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4) if not ordered else None}
+        if ordered:
+            roof["sp_kernel_note"] = ("ordered launches: the HIP events bracket the TM launch only; the SP kernel "
+                                      "(sp_step_ord_kernel) and ord_sort_kernel before it are untimed here (their "
+                                      "rocprofv3 kernel-trace averages are in profiles/<round>/kernel_stats.csv) "
+                                      "but inside ms_per_step")
         if c4:
             # a fleet's streams share one model: its index and records are read
             # from the XCD L2s and the Infinity Cache, so the bytes the kernel
@@ -674,7 +766,7 @@ def main():
                    "shape": args.shape,
                    "mode": ("lockstep: one htm_step per step, every stream advances one network.run(1) per step"
                             + (" (ordered: SP kernel, cost-ordered stream list, TM steps heaviest first)"
-                               if args.ordered == "on" and S <= 16384 and not c3 else "")
+                               if ordered else "")
                             if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
                    "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered,
@@ -692,6 +784,8 @@ def main():
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
         ("run_mode" if args.mode == "step" else "lockstep"): other,
     }
+    if tp_rec is not None:
+        out["test_phase"] = tp_rec
     if rank == 0 and world == 1 and not args.no_cpu and not c3 and not c4 and args.shape == "model1":
         out["cpu_baseline"] = cpu_baseline(trace, train_vals, n_total)
     eng.close()
@@ -711,6 +805,32 @@ PMC_PASSES = {
     "pmc_wr": ["WRITE_SIZE", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"],
 }
 PMC_L2_PASS = {"pmc_l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum"]}
+# where the waves' cycles go (SQ block: 8 counters per pass, SQ_WAVE_CYCLES in
+# each so every pass normalises itself): issuing / parked on s_waitcnt or
+# s_barrier / ready but not issued, per-unit issue, LDS bank conflicts
+PMC_SQ_PASSES = {
+    "pmc_sq1": ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"],
+    "pmc_sq2": ["SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_FLAT",
+                "SQ_WAIT_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_VALU"],
+    "pmc_sq3": ["SQ_WAVE_CYCLES", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                "SQ_INST_LEVEL_VMEM", "SQ_INSTS_BRANCH", "SQ_ACTIVE_INST_MISC"],
+}
+SQ_LEARN_STEPS = 48  # the learn leg's SQ passes time this many steps (after its warm-up): fractions, not bytes
+
+
+def issue_record(k):
+    """roofline.issue: the SQ fractions of the dominant kernel's wave-cycles."""
+    sq = (k or {}).get("sq")
+    if not sq:
+        return None
+    keys = ("issue_active", "waiting", "issue_stalled", "valu", "salu", "lds", "vmem", "flat", "lds_issue_stalled",
+            "lds_bank_conflict_over_lds_active", "cycles_per_wave", "waves")
+    rec = {x: sq.get(x) for x in keys if sq.get(x) is not None}
+    rec["basis"] = ("rocprofv3 SQ counter passes of this workload (median per dispatch): fractions of SQ_WAVE_CYCLES; "
+                    "waiting = SQ_WAIT_ANY (parked on s_waitcnt for memory / LDS or on s_barrier), issue_stalled = "
+                    "SQ_WAIT_INST_ANY, issue_active = SQ_ACTIVE_INST_ANY")
+    return rec
 
 
 def self_pmc_passes(args, steps=128, learn_leg=False):
@@ -728,13 +848,13 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
         return None, "rocprofv3 not found: traffic not measured"
     out = tempfile.mkdtemp(prefix="htm_pmc_", dir="/tmp")
     if learn_leg:
-        child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "3", "--steps", "16", "--warmup",
-                 str(args.learn_warmup), "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", "step",
-                 "--streams", str(args.learn_streams)]
+        child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "3", "--steps", str(args.learn_steps),
+                 "--warmup", str(args.learn_warmup), "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", "step",
+                 "--streams", str(args.learn_streams), "--split-learn", args.split_learn]
     else:
         child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
                  "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode,
-                 "--no-learn-on", "--shape", args.shape]
+                 "--no-learn-on", "--no-test-phase", "--shape", args.shape]
         if args.flush_mode != "auto":
             child += ["--flush-mode", args.flush_mode]
         if args.ordered != "on":
@@ -747,10 +867,14 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
     passes = dict(PMC_PASSES)
     if args.config == 4 and not learn_leg:
         passes.update(PMC_L2_PASS)  # the fleet's shared model is read from L2: its hit rate
+    passes.update(PMC_SQ_PASSES)
     for name, counters in passes.items():
         t0 = time.time()
+        cc = list(child)
+        if learn_leg and name in PMC_SQ_PASSES:  # fractions: a shorter region of the same workload
+            cc[cc.index("--steps") + 1] = str(min(args.learn_steps, SQ_LEARN_STEPS))
         cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", os.path.join(out, "run", name), "-o", "run",
-               "--", *child]
+               "--", *cc]
         try:
             r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=420)
         except subprocess.TimeoutExpired:
@@ -765,21 +889,45 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
     return path, None
 
 
-def kernel_name(c3, c4, fused):
+SP_LEARN_KERNEL = "sp_step_ord_kernel<true, true>"  # the split learning step's SP kernel (paged permanences)
+
+
+def kernel_name(c3, c4, fused, split=False):
     """The dominant kernel's name as rocprofv3 reports it (without the
-    argument list): the fused SP+TM kernel, frozen-TM or learning variant."""
+    argument list): the fused SP+TM kernel, frozen-TM or learning variant
+    (split learning steps: the TM-only learning kernel)."""
     if not fused:
         return "tm_step_kernel<false, true>" if not c3 else "tm_step_kernel<true, false>"
-    return "htm_run_kernel<true>" if c3 else "htm_run_frozen_kernel"
+    if c3:
+        return "htm_run_tmlearn_kernel" if split else "htm_run_kernel<true>"
+    return "htm_run_frozen_kernel"
 
 
-def timed_replay(eng, vals, scores, a, steps, mode, chunk, gather, gathered, rank, world, device):
+def split_traffic(path, split, tm_kernel):
+    """HBM bytes per learning step from the counter passes: the TM kernel's,
+    plus the SP kernel's for a split step; (bytes, TM kernel record)."""
+    k = pmc_kernel(path, tm_kernel)
+    if not k or "hbm_bytes_per_dispatch" not in k:
+        return None, k
+    b = k["hbm_bytes_per_dispatch"]
+    if split:
+        ks = pmc_kernel(path, SP_LEARN_KERNEL)
+        if not ks or "hbm_bytes_per_dispatch" not in ks:
+            return None, k
+        b += ks["hbm_bytes_per_dispatch"]
+    return int(b), k
+
+
+def timed_replay(eng, vals, scores, a, steps, mode, chunk, gather, gathered, rank, world, device, marks=None):
     """Steps [a, a + steps) of every stream, timed between barrier +
     synchronize on both sides, the max over ranks returned (the bench
     contract).  mode "step": one eng.step per step (lockstep) and, with N>1
     ranks, each step's scores gathered to rank 0 (SLO alerting input);
     "run": eng.run chunks of `chunk` steps, one gather_rows per chunk,
-    overlapped with the next chunk.  Returns (seconds, gathered)."""
+    overlapped with the next chunk.  marks (lockstep only): a list that gets a
+    HIP event recorded on the step stream before step 0 and after every 64th
+    step (and the last) -- the per-window breakdown of a long region.  Returns
+    (seconds, gathered)."""
     import torch
     import torch.distributed as dist
     import _pkg
@@ -800,8 +948,14 @@ def timed_replay(eng, vals, scores, a, steps, mode, chunk, gather, gathered, ran
                                           staging=gathered[:, c0_:c0_ + m] if rank == 0 else None)
                 handles.append(h)
     else:
+        if marks is not None and cuda:
+            marks.append((0, torch.cuda.Event(enable_timing=True)))
+            marks[-1][1].record()
         for k in range(steps):
             eng.step(vals[a + k], out=scores[a + k])
+            if marks is not None and cuda and ((k + 1) % 64 == 0 or k + 1 == steps):
+                marks.append((k + 1, torch.cuda.Event(enable_timing=True)))
+                marks[-1][1].record()
             if gather is not None:
                 h, _ = gather.gather(scores[a + k], staging=gathered[k] if rank == 0 else None)
                 handles.append(h)

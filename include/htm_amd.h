@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HTM_ABI_VERSION 4
+#define HTM_ABI_VERSION 5
 
 /* error codes */
 #define HTM_OK 0
@@ -189,6 +189,10 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    writes (0: the default, 8, at most half the log ring); a cadence past
                                    the ring makes the log fill, and a full log makes a step count its
                                    discarded phase 2s in full (results identical) */
+#define HTM_OPT_SPLIT_LEARN 14  /* 1 (default): a lockstep htm_step with TM learning on runs the SP kernel (its
+                                   learning included) and then the TM learning kernel with the SP compiled out
+                                   (each at its own occupancy); results are identical.  0: one fused SP+TM
+                                   learning kernel */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued
@@ -248,6 +252,10 @@ int htm_run_sdr(htm_engine* eng, int32_t n_steps, const uint32_t* d_sdr, float* 
 #define HTM_OUT_BUCKETS 10         /* int32 [4] the encoders' bucket index per field of the last
                                       record (-1: missing value): the sensor's bucketIdxOut
                                       (NetworkModel.py:88-95) */
+#define HTM_OUT_PRED_COLS 11       /* uint8 [ncol]  nonzero(colConfidence t): the predicted columns the
+                                      next step's raw anomaly reads (NetworkModel.py:133 via
+                                      prevPredictedColumns); read from the packed state, the
+                                      state is not changed (HTM_OUT_COL_CONFIDENCE densifies it) */
 int htm_get_output(htm_engine* eng, int32_t which, void* d_dst, size_t bytes, void* stream);
 /* Bytes per stream of an output selector (0 if unknown). */
 size_t htm_output_bytes(const htm_engine* eng, int32_t which);

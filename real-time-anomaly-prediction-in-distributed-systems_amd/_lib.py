@@ -30,7 +30,7 @@ HTM_E_IO = -4
 HTM_E_STATE = -5
 
 OUT = dict(active_columns=1, prev_pred_columns=2, inf_active=3, inf_predicted=4, lrn_active=5,
-           lrn_predicted=6, col_confidence=7, tm_output=8, sp_overlaps=9, buckets=10)
+           lrn_predicted=6, col_confidence=7, tm_output=8, sp_overlaps=9, buckets=10, pred_columns=11)
 # sp_perm_ckpt first: a paged engine imports its permanences against the
 # initial values of the checkpoints they came with (HTM_ST_SP_PERM_CKPT)
 ST = dict(sp_perm_ckpt=17, sp_connT=1, sp_potmask=2, sp_perm=3, sp_duty=4, sp_scalars=5, tm_header=6, tm_bitmaps=7,
@@ -49,6 +49,7 @@ OPT_DEFER_DUTY = 10
 OPT_FLUSH_MODE = 11
 OPT_ORDERED = 12
 OPT_FLUSH_EVERY = 13
+OPT_SPLIT_LEARN = 14
 
 
 class HtmConfig(ctypes.Structure):

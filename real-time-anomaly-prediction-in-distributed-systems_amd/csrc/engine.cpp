@@ -110,6 +110,7 @@ struct htm_engine {
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
     bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
     int32_t ordered = 1;              // HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first
+    int32_t split_learn = 1;          // HTM_OPT_SPLIT_LEARN: learning lockstep steps run the SP kernel, then TM-only
     uint32_t* ord = nullptr;          // [n] the ordered launch's stream of each workgroup
     uint16_t* ord_est = nullptr;      // [n] each stream's TM cost estimate (sp_step_ord_kernel)
     unsigned long long* wg_trace = nullptr;  // A/B builds: HTM_WG_TRACE timeline of the latest lockstep launch
@@ -541,7 +542,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     }
     if (!r) r = check_lds(e->dc);
     if (!r) r = allocate(e);
-    if (!r) r = grow_enc(e, (size_t)e->run_chunk, nullptr);  // RDSE engines: capacity failures show up here
+    if (!r) r = grow_enc(e, 1, nullptr);  // RDSE engines: one step's lists now (longer launches grow them)
     if (!r && tm_configure_lds(e->dc)) {
         size_t mx = std::max(tm_step_lds_bytes(e->dc, 0, 1),
                              std::max(tm_step_lds_bytes(e->dc, 1, 0), tm_step_lds_bytes(e->dc, 0, 0)));
@@ -657,6 +658,7 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         e->flush_mode = value;
     }
     else if (opt == HTM_OPT_ORDERED) e->ordered = value ? 1 : 0;
+    else if (opt == HTM_OPT_SPLIT_LEARN) e->split_learn = value ? 1 : 0;
     else if (opt == HTM_OPT_FLUSH_EVERY) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "flush cadence: 0 (default) or N >= 1 lockstep steps");
         if (int r = flush_sync(e)) return r;
@@ -704,6 +706,10 @@ static int alloc_dlog(htm_engine* e) {
     ALLOC(e->tm.fx_dupto, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
     ALLOC(e->tm.fx_fwork, uint32_t, 4);
+    // a split job's id is (stream * fx_dcap + slot) * (fx_nwin + 1) + window (uint32)
+    if (S * (size_t)d.fx_dcap * ((size_t)d.fx_nwin + 1) >= ((size_t)1 << 32))
+        return htm_fail(HTM_E_CAPACITY, "deferred-write flush: %zu streams x %d ring slots x %d windows overflow the "
+                        "32-bit job ids", S, d.fx_dcap, d.fx_nwin + 1);
     ALLOC(e->tm.fx_fjobs, uint32_t, S * (size_t)d.fx_dcap * (size_t)d.fx_nwin);
     if (e->flush_prio) {
         int least = 0, greatest = 0;
@@ -862,9 +868,10 @@ static int prepare_step(htm_engine* e, hipStream_t st, int* frozen) {
 
 // RDSE engines: the encoder kernel runs the streams' encoders through the
 // launch's n_steps records first.  Their lists (count + n_fields * enc_w bits,
-// DevCfg::enc_list words per stream-step) are allocated at creation for
-// run_chunk steps (the longest fused launch of htm_run); a caller that raises
-// run_chunk grows the buffer (synchronising) on the next longer launch.
+// DevCfg::enc_list words per stream-step) are allocated at creation for one
+// step (a lockstep engine never needs more; a 131,072-stream model.yaml fleet
+// would hold 1.6 GB for run_chunk steps); the first longer launch grows the
+// buffer (synchronising) to its length.
 static int grow_enc(htm_engine* e, size_t steps, hipStream_t st) {
     if (e->dc.enc_type != HTM_ENC_RDSE || steps <= e->enc_cap) return HTM_OK;
     const size_t per = (size_t)e->n * e->dc.enc_list * 2;
@@ -896,15 +903,21 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     // ordered lockstep step (HTM_OPT_ORDERED; frozen, one step, dense SP, at
     // most 16,384 streams): the SP kernel, the cost-ordered stream list, then
     // the fused kernel's TM steps in that order
-    const bool ordered = frozen && n_steps == 1 && !e->tm_learn && e->ordered && !e->dc.sp_paged && e->n <= 16384;
+    const bool ordered = frozen && n_steps == 1 && !e->tm_learn && e->ordered && !e->dc.sp_paged && e->n <= ORD_MAX_STREAMS;
+    // split learning step (HTM_OPT_SPLIT_LEARN; TM learning on, one step): the
+    // SP kernel (its learning, paged rows included, at the SP kernel's own
+    // occupancy), then the TM-only learning kernel (the SP compiled out)
+    const bool split = e->tm_learn && n_steps == 1 && e->split_learn && !e->dc.sdr_in;
     if (prof) {
         int r = next_events(e, ev, n_steps);
         if (r) return r;
         // one event before and one after the fused kernel (an event record is
         // a few microseconds of the queue's time: no empty "SP" interval);
-        // ordered: around the TM launch only (its SP kernel and sort untimed)
-        e->ev_fused.back() = 1;
-        if (!ordered) HIP_TRY(hipEventRecord(ev[1], st));
+        // ordered: around the TM launch only (its SP kernel and sort untimed);
+        // split learning: the SP kernel and the TM kernel each
+        e->ev_fused.back() = split ? 0 : 1;
+        if (split) HIP_TRY(hipEventRecord(ev[0], st));
+        else if (!ordered) HIP_TRY(hipEventRecord(ev[1], st));
     }
     // auto unit: a stream keeps its TM state in LDS for a unit's steps; longer
     // units save state round trips and queue handoffs, shorter ones balance
@@ -923,6 +936,11 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         if (launch_ord_sort(e->dc, e->ord_est, e->ord, e->n, st)) return htm_fail(HTM_E_HIP, "ord_sort launch");
         if (prof) HIP_TRY(hipEventRecord(ev[1], st));  // (the TM launch's start)
         tb.ord = e->ord;
+        tb.tm_only = 1;
+    } else if (split) {
+        if (launch_sp_step_ord(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, nullptr, nullptr, st))
+            return htm_fail(HTM_E_HIP, "sp_step launch");
+        if (prof) HIP_TRY(hipEventRecord(ev[1], st));
         tb.tm_only = 1;
     }
     // deferred dutyCycle() writes: frozen lockstep launches (one step)
@@ -1147,6 +1165,12 @@ __global__ void out_kernel(DevCfg c, SpBufs sp, TmBufs tm, int which, uint8_t* d
         uint32_t* o = reinterpret_cast<uint32_t*>(dst) + (size_t)s * c.cw;
         const uint32_t* bm = tm.bm + (size_t)s * 4 * c.cw;
         for (int i = threadIdx.x; i < c.cw; i += blockDim.x) o[i] = bm[i] | bm[c.cw + i];
+    } else if (which == HTM_OUT_PRED_COLS) {
+        uint8_t* o = dst + (size_t)s * c.ncol;
+        const uint32_t* nz = tm.colnz + (size_t)s * (c.nw + 1);
+        const bool packed = nz[c.nw] == 1u;  // the bitmap is current (else the dense copy is)
+        for (int i = threadIdx.x; i < c.ncol; i += blockDim.x)
+            o[i] = packed ? (uint8_t)((nz[i >> 5] >> (i & 31)) & 1u) : (tm.colconf[(size_t)s * c.ncol + i] != 0.0f ? 1 : 0);
     }
 }
 
@@ -1171,7 +1195,8 @@ size_t htm_output_bytes(const htm_engine* e, int32_t which) {
     const DevCfg& d = e->dc;
     switch (which) {
         case HTM_OUT_ACTIVE_COLUMNS:
-        case HTM_OUT_PREV_PRED_COLS: return (size_t)d.ncol;
+        case HTM_OUT_PREV_PRED_COLS:
+        case HTM_OUT_PRED_COLS: return (size_t)d.ncol;
         case HTM_OUT_INF_ACTIVE:
         case HTM_OUT_INF_PREDICTED:
         case HTM_OUT_LRN_ACTIVE:
@@ -1195,6 +1220,7 @@ int htm_get_output(htm_engine* e, int32_t which, void* d_dst, size_t bytes, void
         case HTM_OUT_ACTIVE_COLUMNS:
         case HTM_OUT_PREV_PRED_COLS:
         case HTM_OUT_TM_OUTPUT:
+        case HTM_OUT_PRED_COLS:
             if (which == HTM_OUT_PREV_PRED_COLS && !e->keep_prev)
                 return htm_fail(HTM_E_STATE, "prev-predicted columns need htm_set_option(KEEP_PREV)");
             hipLaunchKernelGGL(out_kernel, dim3(e->n), dim3(256), 0, st, d, e->sp, e->tm, which, (uint8_t*)d_dst);

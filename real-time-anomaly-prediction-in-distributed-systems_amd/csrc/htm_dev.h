@@ -221,6 +221,7 @@ struct TmBufs {
     int32_t tm_only;               // 1: the launch skips the SP (ordered launches)
 };
 #define ORD_NB 64                  // cost buckets of the ordering (active-cell estimate / (max_act_cells / 64))
+#define ORD_MAX_STREAMS 16384      // ordered lockstep launches: ord_sort_kernel's one workgroup (n bytes of LDS)
 
 // deferred-log flush error flags (fx_fwork[1]; htm_status / htm_counters)
 #define FX_ERR_QCAP 16u   // a replayed phase 2 overflowed q_cap (as in the step: results invalid)

@@ -287,19 +287,23 @@ __global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const 
     sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps, LEARN ? bkey : nullptr, enc);
 }
 
-// The SP of an ordered lockstep step (HTM_OPT_ORDERED, dense SP): the fused
-// kernel's four-wave SP, then the stream's TM cost estimate -- the active cells
-// TM phase 1 will list: a predicted column's predicted cells in
-// infPredictedState(t-1) (tm_bm), all K cells of a bursting one -- to est[s]
-// for ord_sort_kernel.
-template <bool LEARN>
+// The SP of a split lockstep step, the fused kernel's four-wave SP (its
+// learning staged through the overlap planes) as a kernel of its own:
+//  * ordered frozen steps (HTM_OPT_ORDERED, dense SP): then the stream's TM
+//    cost estimate -- the active cells TM phase 1 will list: a predicted
+//    column's predicted cells in infPredictedState(t-1) (tm_bm), all K cells
+//    of a bursting one -- to est[s] for ord_sort_kernel;
+//  * learning steps (HTM_OPT_SPLIT_LEARN; PAGED: paged permanences): est is
+//    null and the TM-only learning kernel follows.
+template <bool LEARN, bool PAGED>
 __global__ __launch_bounds__(256) void sp_step_ord_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps,
                                                           const uint16_t* enc, const uint32_t* tm_bm, uint16_t* est) {
     __shared__ SpShared sh;
     __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
     __shared__ uint32_t planes[SP_PLANE_WORDS];
     const int s = blockIdx.x;
-    sp_step_body<LEARN, false, true>(c, b, values, s, sh, write_overlaps, LEARN ? bkey : nullptr, enc, planes);
+    sp_step_body<LEARN, PAGED, true>(c, b, values, s, sh, write_overlaps, LEARN ? bkey : nullptr, enc, planes);
+    if (!est) return;
     __syncthreads();
     if (wave_id() == 0) {
         const int K = c.K, a = lane_id();
@@ -318,12 +322,15 @@ __global__ __launch_bounds__(256) void sp_step_ord_kernel(DevCfg c, SpBufs b, co
 int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                        const uint32_t* tm_bm, uint16_t* est, hipStream_t st) {
     const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? b.enc_in : nullptr;  // (one step: row 0)
-    if (learn)
-        hipLaunchKernelGGL(sp_step_ord_kernel<true>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps, enc,
-                           tm_bm, est);
+    if (learn && c.sp_paged)
+        hipLaunchKernelGGL((sp_step_ord_kernel<true, true>), dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps,
+                           enc, tm_bm, est);
+    else if (learn)
+        hipLaunchKernelGGL((sp_step_ord_kernel<true, false>), dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps,
+                           enc, tm_bm, est);
     else
-        hipLaunchKernelGGL(sp_step_ord_kernel<false>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps, enc,
-                           tm_bm, est);
+        hipLaunchKernelGGL((sp_step_ord_kernel<false, false>), dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps,
+                           enc, tm_bm, est);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -739,6 +739,9 @@ __device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b
     const int pw = c.nin_pad >> 5;
     const size_t ms = (size_t)model_stream(c, s);
     const uint32_t* prow = b.potmask + (ms * c.ncol + col) * pw;
+    // the first chunk's potential-mask word is loaded before the row lookup
+    // (independent round trips in flight together)
+    uint32_t pword = (l >> 2) < pw ? prow[l >> 2] : 0u;
     float* perm = sp_perm_row<PAGED_OK, LDSBUF>(c, b, s, col, scratch);
     if (!perm) return;
     uint32_t* connT = b.connT + ms * c.nin_pad * c.nw;
@@ -748,26 +751,155 @@ __device__ __forceinline__ void sp_adapt_column(const DevCfg& c, const SpBufs& b
         int wi = chunk + (l >> 2);
         uint32_t byte = 0, ibyte = 0;
         if (wi < pw) {
-            byte = (prow[wi] >> ((l & 3) * 8)) & 0xFFu;
+            if (chunk) pword = prow[wi];
+            byte = (pword >> ((l & 3) * 8)) & 0xFFu;
             ibyte = (in_bits[wi] >> ((l & 3) * 8)) & 0xFFu;
         }
-        uint32_t pc = __popc(byte);
-        uint32_t incl = wave_incl_scan(pc);
-        uint32_t r = rank_base + incl - pc;
-        for (uint32_t x = byte; x; x &= x - 1) {
-            int j = __ffs(x) - 1;
-            int input = (chunk + (l >> 2)) * 32 + (l & 3) * 8 + j;
-            float p = perm[r];
-            bool oldc = p >= c.sp_conn_thr;
-            if (mode == 0) p = p + (((ibyte >> j) & 1u) ? c.sp_inc : -1 * c.sp_dec);
-            else p = p + c.sp_below_inc;
-            bool newc;
-            p = sp_update_perm(c, p, mode == 0, newc);
-            perm[r] = p;
-            if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
-            r++;
+        const uint32_t pc = __popc(byte);
+        const uint32_t incl = wave_incl_scan(pc);
+        const uint32_t r0 = rank_base + incl - pc;
+        // the lane's (<= 8, consecutive) permanences: every load issued before
+        // any is used -- one HBM round trip per chunk, not one per synapse
+        float pv[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) pv[k] = (uint32_t)k < pc ? perm[r0 + k] : 0.0f;
+        uint32_t x = byte;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if ((uint32_t)k < pc) {
+                const int j = __ffs(x) - 1;
+                x &= x - 1;
+                const int input = (chunk + (l >> 2)) * 32 + (l & 3) * 8 + j;
+                float p = pv[k];
+                const bool oldc = p >= c.sp_conn_thr;
+                if (mode == 0) p = p + (((ibyte >> j) & 1u) ? c.sp_inc : -1 * c.sp_dec);
+                else p = p + c.sp_below_inc;
+                bool newc;
+                p = sp_update_perm(c, p, mode == 0, newc);
+                perm[r0 + k] = p;
+                if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
+            }
         }
         rank_base += lane63(incl);
+    }
+}
+
+// The same for the columns of one wave -- list[w], list[w + NW], ... (w =
+// wave_id(), NW waves) -- with inputs of one 512-input chunk (nin_pad <= 512)
+// and a 512-word LDS scratch for the wave (the fused kernels' overlap planes,
+// free while adapting).  Software-pipelined: the pool rows of up to 64 of the
+// wave's columns are looked up in one round trip (paged), and a column's
+// potential-mask word and whole permanence row (coalesced 16-byte loads) are
+// loaded while the previous column is updated; the row is staged through the
+// scratch so each lane reads its (<= 8, consecutive) permanences by rank.  A
+// column without a pool row (paged) regenerates its initial values first
+// (sp_perm_row) and is loaded unpipelined.  Results equal sp_adapt_column's.
+template <bool PAGED_OK>
+__device__ __forceinline__ void sp_adapt_wave(const DevCfg& c, const SpBufs& b, int s, const uint16_t* list, int n,
+                                              const uint32_t* in_bits, int mode, uint32_t* scratch) {
+    const int l = lane_id(), w = wave_id(), nwv = blockDim.x >> 6;
+    const int nk = n > w ? (n - w + nwv - 1) / nwv : 0;
+    if (nk <= 0) return;
+    const size_t ms = (size_t)model_stream(c, s);
+    const int pw = c.nin_pad >> 5;
+    const int npot = c.n_potential;
+    const bool paged = PAGED_OK && c.sp_paged;
+    uint32_t* connT = b.connT + ms * c.nin_pad * c.nw;
+    // inputs of this lane: word l >> 2, byte l & 3
+    const uint32_t ibyte = (l >> 2) < pw ? (in_bits[l >> 2] >> ((l & 3) * 8)) & 0xFFu : 0u;
+    float4* const st4 = reinterpret_cast<float4*>(scratch);
+    // 16-byte row loads: pool rows are 128-byte aligned, dense rows when npot % 4 == 0
+    const bool vec = paged || (npot & 3) == 0;
+    for (int k0 = 0; k0 < nk; k0 += 64) {
+        const int kn = nk - k0 < 64 ? nk - k0 : 64;
+        uint32_t mycol = 0u, myrow = SP_ROW_NONE;
+        if (l < kn) {
+            mycol = list[w + (k0 + l) * nwv];
+            if (paged) myrow = b.prow[ms * c.ncol + mycol];
+        }
+        // stage of column j: its row pointer (null: a fresh paged column, loaded
+        // after its regeneration), potential-mask word and row values
+        auto rowp = [&](int j) -> const float* {
+            const uint32_t col = (uint32_t)__builtin_amdgcn_readlane((int)mycol, j);
+            if (!paged) return b.perm + (ms * c.ncol + col) * (size_t)npot;
+            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)myrow, j);
+            return r == SP_ROW_NONE ? nullptr : b.pool + (size_t)r * c.pool_stride;
+        };
+        auto load = [&](int j, const float* row, uint32_t& pword, float4& v0, float4& v1) {
+            const uint32_t col = (uint32_t)__builtin_amdgcn_readlane((int)mycol, j);
+            const uint32_t* prow = b.potmask + (ms * c.ncol + col) * pw;
+            pword = (l >> 2) < pw ? prow[l >> 2] : 0u;
+            const int i0 = 8 * l;
+            v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i0 + 8 <= npot && vec) {
+                v0 = *reinterpret_cast<const float4*>(row + i0);
+                v1 = *reinterpret_cast<const float4*>(row + i0 + 4);
+            } else if (i0 < npot) {
+                float x[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) x[q] = i0 + q < npot ? row[i0 + q] : 0.f;
+                v0 = make_float4(x[0], x[1], x[2], x[3]);
+                v1 = make_float4(x[4], x[5], x[6], x[7]);
+            }
+        };
+        uint32_t pw_c = 0u;
+        float4 a0, a1;
+        const float* row_c = rowp(0);
+        if (row_c) load(0, row_c, pw_c, a0, a1);
+        for (int j = 0; j < kn; j++) {
+            const uint32_t col = (uint32_t)__builtin_amdgcn_readlane((int)mycol, j);
+            float* row = const_cast<float*>(row_c);
+            if (!row) {  // paged, no pool row yet: regenerate the initial values, then load
+                row = sp_perm_row<PAGED_OK, true>(c, b, s, (int)col, scratch);
+                if (row) load(j, row, pw_c, a0, a1);
+            }
+            // the next column's loads go out before this column is updated
+            uint32_t pw_n = 0u;
+            float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+            const float* row_n = nullptr;
+            if (j + 1 < kn) {
+                row_n = rowp(j + 1);
+                if (row_n) load(j + 1, row_n, pw_n, b0, b1);
+            }
+            if (row) {
+                // stage the row, then each lane takes its ranks
+                st4[2 * l] = a0;
+                st4[2 * l + 1] = a1;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const uint32_t byte = (pw_c >> ((l & 3) * 8)) & 0xFFu;
+                const uint32_t pc = __popc(byte);
+                const uint32_t incl = wave_incl_scan(pc);
+                const uint32_t r0 = incl - pc;
+                const float* sf = reinterpret_cast<const float*>(scratch);
+                float pv[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) pv[k] = (uint32_t)k < pc ? sf[r0 + k] : 0.0f;
+                const uint32_t cw = col >> 5, cb = 1u << (col & 31);
+                uint32_t x = byte;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    if ((uint32_t)k < pc) {
+                        const int jb = __ffs(x) - 1;
+                        x &= x - 1;
+                        const int input = (l >> 2) * 32 + (l & 3) * 8 + jb;
+                        float p = pv[k];
+                        const bool oldc = p >= c.sp_conn_thr;
+                        if (mode == 0) p = p + (((ibyte >> jb) & 1u) ? c.sp_inc : -1 * c.sp_dec);
+                        else p = p + c.sp_below_inc;
+                        bool newc;
+                        p = sp_update_perm(c, p, mode == 0, newc);
+                        row[r0 + k] = p;
+                        if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // (the scratch is restaged next)
+            }
+            row_c = row_n;
+            pw_c = pw_n;
+            a0 = b0;
+            a1 = b1;
+        }
     }
 }
 
@@ -875,8 +1007,12 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     constexpr bool LB = PLANES && std::is_same<SH, SpShared>::value;  // (PLANES: the fused kernels' planes)
     static_assert(!LB || (TM_NT / 64) * 512 <= SP_PLANE_WORDS, "replay scratch: 512 words per wave");
     uint32_t* scratch = LB ? planes + wave_id() * 512u : nullptr;
-    for (int a = wave_id(); a < nact; a += blockDim.x >> 6)
-        sp_adapt_column<PAGED_OK, LB>(c, b, s, sh.actlist[a], sh.in, 0, scratch);
+    if (LB && c.nin_pad <= 512 && c.n_potential <= 512) {
+        sp_adapt_wave<PAGED_OK>(c, b, s, sh.actlist, nact, sh.in, 0, scratch);
+    } else {
+        for (int a = wave_id(); a < nact; a += blockDim.x >> 6)
+            sp_adapt_column<PAGED_OK, LB>(c, b, s, sh.actlist[a], sh.in, 0, scratch);
+    }
     __syncthreads();
     // ---- updateDutyCycles_ (period = min(dutyCyclePeriod, iterationNum))
     float* odc = b.duty + (size_t)model_stream(c, s) * 2 * c.ncol;
@@ -909,8 +1045,12 @@ __device__ __forceinline__ void sp_step_body(const DevCfg& c, const SpBufs& b, c
     const int nb = sh.nbump;
     if (nb > 0) {
         // ascending order is irrelevant: each column is updated independently
-        for (int k = wave_id(); k < nb; k += blockDim.x >> 6)
-            sp_adapt_column<PAGED_OK, LB>(c, b, s, sh.bump[k], sh.in, 1, scratch);
+        if (LB && c.nin_pad <= 512 && c.n_potential <= 512) {
+            sp_adapt_wave<PAGED_OK>(c, b, s, sh.bump, nb, sh.in, 1, scratch);
+        } else {
+            for (int k = wave_id(); k < nb; k += blockDim.x >> 6)
+                sp_adapt_column<PAGED_OK, LB>(c, b, s, sh.bump[k], sh.in, 1, scratch);
+        }
     }
     // ---- isUpdateRound_: updateMinDutyCyclesGlobal_
     if (sh.iter % (uint32_t)c.update_period == 0) {

@@ -39,16 +39,20 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     const int total = (int)(n * nblk);
     // a single unit per stream runs on the hardware dispatcher (grid = streams)
     if (nblk > 1 && hipMemsetAsync(wq, 0, ((size_t)n + 1) * sizeof(uint32_t), st) != hipSuccess) return -1;
-    const int which = tm_learn ? 0 : frozen ? (c.sp_paged ? 2 : sp_learn ? 4 : 1) : 3;
+    // a TM-only launch (ordered lockstep steps: the SP kernel ran first, with
+    // its learning) needs no SP code: the inference-only frozen kernel
+    const int which = tm_learn ? (b.tm_only ? 5 : 0)
+                               : frozen ? (c.sp_paged ? 2 : (sp_learn && !b.tm_only) ? 4 : 1) : 3;
     const void* fn = which == 0 ? tmk_fn_run_learn() : which == 1 ? tmk_fn_run_frozen()
                      : which == 2 ? tmk_fn_run_frozen_paged() : which == 4 ? tmk_fn_run_frozen_spl()
-                                                                              : tmk_fn_run_infer();
+                     : which == 5 ? tmk_fn_run_learn_tm() : tmk_fn_run_infer();
     const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
     switch (which) {
         case 0: return tmk_launch_run_learn(grid, lds, st, HTM_RUN_PASS);
         case 1: return tmk_launch_run_frozen(grid, lds, st, HTM_RUN_PASS);
         case 2: return tmk_launch_run_frozen_paged(grid, lds, st, HTM_RUN_PASS);
         case 4: return tmk_launch_run_frozen_spl(grid, lds, st, HTM_RUN_PASS);
+        case 5: return tmk_launch_run_learn_tm(grid, lds, st, HTM_RUN_PASS);
         default: return tmk_launch_run_infer(grid, lds, st, HTM_RUN_PASS);
     }
 }
@@ -325,7 +329,7 @@ int tm_configure_lds(const DevCfg& c) {
     size_t b0 = tm_step_lds_bytes(c, 1, 0), b1 = tm_step_lds_bytes(c, 0, 1), b2 = tm_step_lds_bytes(c, 0, 0);
     int r = tmk_attr_step(b0, b1, b2);
     r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1) |
-         tmk_attr_run_frozen_spl(b1);
+         tmk_attr_run_frozen_spl(b1) | tmk_attr_run_learn_tm(b0);
     r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
                  hipSuccess ? 0 : -1;
     (void)hipGetLastError();
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(1024) void ord_sort_kernel(DevCfg c, const uint16_t
 }
 
 int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st) {
-    if (n <= 0 || n > 65536) return -1;
+    if (n <= 0 || n > ORD_MAX_STREAMS) return -1;  // (n + 512 bytes of LDS)
     hipLaunchKernelGGL(ord_sort_kernel, dim3(1), dim3(1024), (size_t)n, st, c, est, ord, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -111,7 +111,11 @@ enum {
     // updates, wave 0's serial adapt / create / update-building, the learn
     // backtrack's state copies, pool compaction, the SP's learning part
     // (adaptSynapses_ incl. paged-row replays, duty cycles, weak-column bumps)
-    SB_LSCAN, SB_LUPD, SB_LW, SB_LBT, SB_COMPACT, SB_SPL
+    SB_LSCAN, SB_LUPD, SB_LW, SB_LBT, SB_COMPACT, SB_SPL,
+    // (round 5) the learning loops split: update building (active-synapse
+    // masks, candidate filters), generator draws (sampling, getCellForNewSegment),
+    // segment writes (adapt, trim, create, queued-update appends)
+    SB_LWB, SB_LWS, SB_LWW
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -120,7 +124,15 @@ enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
 // (SC_HIST .. SC_HIST + 8 are the histogram) learning counts: pool scans and
 // the slots they swept, SP paged-row replays and the lane-0 cycles they took
 // (summed over waves; filled in by htm_debug_stamps from SpBufs::dbg)
-enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC, SC_REPLAYSAMPLE, SC_REPLAYSKIP };
+enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC, SC_REPLAYSAMPLE, SC_REPLAYSKIP,
+       // learning loops: columns of learn phase 1 / 2, sampling calls, draws consumed
+       SC_LP1COLS, SC_LP2COLS, SC_LSAMPLES, SC_LDRAWS };
+
+// learning loops (wave-parallel, round 5): column records per pass (learn
+// phase 1: <= HTM_MAXACT columns; phase 2 in batches) and their LDS words
+// (48-byte records, then each wave's new-source list)
+#define LREC_N 64
+#define LREC_WORDS (LREC_N * 12 + TM_NWAVES * HTM_MAXSYN)
 
 // ---------------------------------------------------------------------------
 // LDS layout
@@ -148,14 +160,15 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     // union of phase-local arrays:
     //  finish: colcnt[ncol] u32, nzcol[ncol] u16, nzstart[ncol+1] u32, and the
     //          qualifying-segment buffers qkey/qdc/skey/sdc[q_lds]
-    //  keys (learning): best-match keys u64[ncol]
+    //  keys (learning): best-match keys u64[ncol], the learning loops' column
+    //          records and new-source lists (LREC_WORDS), phase 2's key columns u16[ncol]
     //  frozen collection: u8 counters[fx_win], active cells u16[max_act_cells],
     //          block prefix u32[max_act_cells+1], list starts u32[max_act_cells],
     //          block -> list map u16[FX_OWN]
     //  trim flags (learning): u32[upd_cap]
     size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
                  (size_t)(c.q_lds + 1) / 2 + (size_t)c.nw;
-    size_t keys = learn ? 2 * (size_t)c.ncol : 0;
+    size_t keys = learn ? 2 * (size_t)c.ncol + LREC_WORDS + ((size_t)c.ncol + 1) / 2 : 0;
     size_t col = frozen ? (size_t)c.fx_win / 4 + 64 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
                               1 + FX_OWN / 2
                         : 0;
@@ -350,14 +363,21 @@ __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA
 // across them).  Only segments with elig(meta) load their rows.  SC_DEPTH
 // batches of 64 segments are in flight per workgroup: meta loads of the
 // batch first, then the row loads, so a pass over the pool costs two HBM
-// round trips per SC_DEPTH x 64 segments.  Returns this thread's bytes.
+// round trips per SC_DEPTH x 64 segments.  SPEC (a scan whose every live
+// segment is eligible: elig must then return true): the rows are loaded with
+// the meta words, not after them -- one round trip per batch; rows of dead
+// slots and lanes past a segment's synapses are loaded and ignored.  Returns
+// this thread's bytes.
+#ifndef SC_DEPTH
 #define SC_DEPTH 8
-template <typename E, typename F>
+#endif
+template <bool SPEC = false, typename E, typename F>
 __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E elig, F f) {
     const uint32_t hwm = t.sh->hwm;
     COUNT(t, SC_NSCAN, 1);
     COUNT(t, SC_SCANSLOTS, hwm);
     const uint32_t g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    const uint32_t cwm1 = (uint32_t)t.c.cw - 1u;
     uint32_t nb = 0;
     for (uint32_t base = 0; base < hwm; base += SC_DEPTH * (TM_NT / 4)) {
         uint32_t m[SC_DEPTH];
@@ -371,10 +391,19 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
 #pragma unroll
         for (int d = 0; d < SC_DEPTH; d++) {
             const uint32_t slot = base + d * (TM_NT / 4) + g;
-            el[d] = meta_live(m[d]) && elig(m[d]);
-            v[d] = make_uint4(0u, 0u, 0u, 0u);
-            if (el[d] && sub * 8u < meta_nsyn(m[d]))
-                v[d] = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
+            if (SPEC) {
+                v[d] = slot < hwm ? *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8)
+                                  : make_uint4(0u, 0u, 0u, 0u);
+            } else {
+                el[d] = meta_live(m[d]) && elig(m[d]);
+                v[d] = make_uint4(0u, 0u, 0u, 0u);
+                if (el[d] && sub * 8u < meta_nsyn(m[d]))
+                    v[d] = *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8);
+            }
+        }
+        if (SPEC) {
+#pragma unroll
+            for (int d = 0; d < SC_DEPTH; d++) el[d] = meta_live(m[d]) && elig(m[d]);
         }
 #pragma unroll
         for (int d = 0; d < SC_DEPTH; d++) {
@@ -385,12 +414,19 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
             if (el[d] && sub * 8u < nsyn) {
                 nb += 16;
                 const uint32_t w[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
+                // all eight state words read unconditionally (one LDS round
+                // trip; a per-synapse `j < nsyn &&` test made a branch and a
+                // wait per read), entries past nsyn clamped into the bitmap and
+                // masked off afterwards
+                uint32_t bits = 0;
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    const uint32_t j = sub * 8 + k;
                     const uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-                    if (j < nsyn && bm_get(state, sid)) mask |= 1u << j;
+                    const uint32_t wi = sid >> 5;
+                    bits |= ((state[wi < cwm1 ? wi : cwm1] >> (sid & 31)) & 1u) << k;
                 }
+                const uint32_t left = nsyn - sub * 8u;
+                mask = (bits & (left >= 8u ? 0xFFu : (1u << left) - 1u)) << (sub * 8u);
             }
             mask |= __shfl_xor(mask, 1, 64);
             mask |= __shfl_xor(mask, 2, 64);
@@ -404,7 +440,7 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
 // `state` by scanning the pool (learning-on form)
 __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
     const uint32_t sub = threadIdx.x & 3;
-    uint32_t nb = scan_pool(t, state, [](uint32_t) { return true; },
+    uint32_t nb = scan_pool<true>(t, state, [](uint32_t) { return true; },
                             [&](uint32_t slot, uint32_t, bool el, uint32_t mask) {
                                 if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) {
                                     const uint32_t i = (uint32_t)atomicAdd(&t.sh->qn, 1);
@@ -716,19 +752,24 @@ __device__ __forceinline__ uint32_t seg_connected_activity(Tm& t, uint32_t slot,
     nb += 4u + 16u * ((nsyn + 7u) / 8u);
     const uint32_t cm = t.conn[slot];
     const uint4* row = reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN);
-    uint32_t n = 0;
+    const uint32_t cwm1 = (uint32_t)t.c.cw - 1u;
+    // the row's used quads loaded before any is read (one round trip), the
+    // state words read unconditionally (entries past nsyn clamped, masked below)
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = (uint32_t)q * 8u < nsyn ? row[q] : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t bits = 0;
+#pragma unroll
     for (int q = 0; q < 4; q++) {
-        if ((uint32_t)q * 8 >= nsyn) break;
-        uint4 v = row[q];
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
         for (int k2 = 0; k2 < 8; k2++) {
-            uint32_t j = q * 8 + k2;
-            uint32_t sid = (w[k2 >> 1] >> ((k2 & 1) * 16)) & 0xFFFFu;
-            if (j < nsyn && ((cm >> j) & 1u) && bm_get(t.infA, sid)) n++;
+            const uint32_t sid = (w[k2 >> 1] >> ((k2 & 1) * 16)) & 0xFFFFu;
+            const uint32_t wi = sid >> 5;
+            bits |= ((t.infA[wi < cwm1 ? wi : cwm1] >> (sid & 31)) & 1u) << (q * 8 + k2);
         }
     }
-    return n;
+    return (uint32_t)__popc(bits & cm & (nsyn >= 32u ? 0xFFFFFFFFu : (1u << nsyn) - 1u));
 }
 
 template <bool FROZEN, typename F>
@@ -1481,22 +1522,25 @@ __device__ __forceinline__ void scan_best(Tm& t, const uint32_t* state, int thr,
     const DevCfg& c = t.c;
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
     const uint32_t sub = threadIdx.x & 3;
-    uint32_t nb = scan_pool(
-        t, state,
-        [&](uint32_t m) {
-            const uint32_t col = col_of(c, meta_cell(m));
-            return !colflags || ((colflags[col >> 5] >> (col & 31)) & 1u);
-        },
-        [&](uint32_t slot, uint32_t m, bool el, uint32_t mask) {
-            const uint32_t n = __popc(mask);
-            if (el && sub == 0 && n >= (uint32_t)thr) {
-                const uint32_t cell = meta_cell(m), col = col_of(c, cell);
-                const uint32_t cic = cell - col * c.K;
-                const unsigned long long key = ((unsigned long long)n << 40) | ((unsigned long long)cic << 32) |
-                                               (unsigned long long)(0xFFFFFFFFu - slot);
-                atomicMax(&keys[col], key);
-            }
-        });
+    auto best = [&](uint32_t slot, uint32_t m, bool el, uint32_t mask) {
+        const uint32_t n = __popc(mask);
+        if (el && sub == 0 && n >= (uint32_t)thr) {
+            const uint32_t cell = meta_cell(m), col = col_of(c, cell);
+            const uint32_t cic = cell - col * c.K;
+            const unsigned long long key = ((unsigned long long)n << 40) | ((unsigned long long)cic << 32) |
+                                           (unsigned long long)(0xFFFFFFFFu - slot);
+            atomicMax(&keys[col], key);
+        }
+    };
+    // every column (learn phase 2): rows loaded with the meta words; flagged
+    // columns only (learn phase 1): rows of those columns' segments only
+    uint32_t nb = colflags ? scan_pool<false>(t, state,
+                                              [&](uint32_t m) {
+                                                  const uint32_t col = col_of(c, meta_cell(m));
+                                                  return ((colflags[col >> 5] >> (col & 31)) & 1u) != 0u;
+                                              },
+                                              best)
+                           : scan_pool<true>(t, state, [](uint32_t) { return true; }, best);
     nb = wg_sum(t.sh, nb);
     if (threadIdx.x == 0) t.sh->bytes += nb;
 }
@@ -1546,6 +1590,7 @@ __device__ __forceinline__ void w_rng_commit(Tm& t, uint32_t y, uint32_t k) {
         fj = fj >= 31u ? fj - 31u : fj;
         sh->rng[fj] = y;
     }
+    COUNT(t, SC_LDRAWS, k);
     if (l == 0) {
         const uint32_t nf = (f + k) % 31u;
         sh->rf = (int32_t)nf;
@@ -1596,6 +1641,169 @@ __device__ __forceinline__ uint64_t w_rng_sample(Tm& t, uint32_t m, uint32_t n) 
     }
 }
 
+// ---- the generator in wave 0's registers for a whole draw pass (round 5:
+// the learning loops' draws).  Lane j < 31 holds the raw sums of the current
+// block of 31 draws (x[n0 + 31 b + j], before the >> 1), `prev` the block
+// before it -- initially the loaded state x[n0 - 31 .. n0 - 1], taken as block
+// -1, fully consumed; pos = draws consumed in the current block.  A block
+// follows from the previous one v by y[j] = v[j] + (j >= 3 ? y[j-3] : v[28+j]):
+// lanes 0..2 get their base v[28 + j] added, then an inclusive scan over
+// stride 3 inside each 16-lane row (DPP row_shr 3, 6, 12: residue classes
+// never mix), and row 0's totals per residue (lanes 15, 13, 14) carried into
+// row 1 by a second such scan -- no LDS round trip (w_rng_peek takes four
+// ds_bpermute's and two LDS reads per block, and commits to LDS).
+// The LDS generator (TmSh::rng, rf, rr) is loaded once and written back once.
+struct WGen {
+    uint32_t cur, prev;  // per lane
+    uint32_t pos;        // draws consumed in the current block (uniform)
+    uint32_t total;      // draws consumed since the load (uniform)
+    uint32_t f0;         // the loaded state's front pointer (uniform)
+};
+
+// v with lane `lane` replaced by the wave-uniform x (v_writelane_b32: no
+// per-lane mask; clang has no builtin for it)
+template <int LANE>
+__device__ __forceinline__ uint32_t writelane_u32(uint32_t v, uint32_t x) {
+    const uint32_t xs = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(xs), "i"(LANE));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wgen_block(uint32_t v) {
+    // lanes 0..2 start from v[j] + v[28 + j] (the recurrence's base), so the
+    // stride-3 scan carries it into every later lane of the residue; no
+    // per-residue lane masks (as loop-invariant SGPR masks they were spilled)
+    uint32_t p = v;
+    p = writelane_u32<0>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 28));
+    p = writelane_u32<1>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 1) + (uint32_t)__builtin_amdgcn_readlane((int)v, 29));
+    p = writelane_u32<2>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 2) + (uint32_t)__builtin_amdgcn_readlane((int)v, 30));
+    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x113, 0xF, 0xF, false);  // row_shr:3
+    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x116, 0xF, 0xF, false);  // row_shr:6
+    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x11C, 0xF, 0xF, false);  // row_shr:12
+    // row 0's totals per residue (lanes 15, 13, 14) enter row 1 at its first
+    // lane of that residue (18, 16, 17) and are carried by the same scan
+    uint32_t q = 0u;
+    q = writelane_u32<16>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 13));
+    q = writelane_u32<17>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 14));
+    q = writelane_u32<18>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 15));
+    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x113, 0xF, 0xF, false);
+    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x116, 0xF, 0xF, false);
+    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x11C, 0xF, 0xF, false);
+    return p + q;
+}
+
+__device__ __forceinline__ WGen wgen_load(Tm& t) {
+    TmSh* sh = t.sh;
+    const uint32_t l = (uint32_t)lane_id();
+    WGen g;
+    g.f0 = (uint32_t)__builtin_amdgcn_readfirstlane(sh->rf);
+    uint32_t fj = g.f0 + l;
+    fj = fj >= 31u ? fj - 31u : fj;
+    g.cur = l < 31u ? sh->rng[fj < 31u ? fj : 0u] : 0u;
+    g.prev = 0u;
+    g.pos = 31u;
+    g.total = 0u;
+    return g;
+}
+
+__device__ __forceinline__ void wgen_ensure(WGen& g) {
+    if (g.pos == 31u) {
+        g.prev = g.cur;
+        g.cur = wgen_block(g.prev);
+        g.pos = 0u;
+    }
+}
+
+// one rng_raw() draw
+__device__ __forceinline__ uint32_t wgen_raw(WGen& g) {
+    wgen_ensure(g);
+    const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)g.cur, (int)g.pos);
+    g.pos++;
+    g.total++;
+    return (y >> 1) & 0x7fffffffu;
+}
+
+// _chooseCellsToLearnFrom's sample of n of the m candidates (m > n >= 1),
+// as w_rng_sample: candidate i is taken when getUInt32(m - i) < n - taken.
+// Within a block the residues are computed across the lanes and the decisions
+// made one TAKEN candidate at a time: the first lane at or past the scan point
+// whose residue is below the remaining count is the next one taken (the lanes
+// before it are not), so a sample costs a ballot per taken candidate instead
+// of a readlane per examined one.
+__device__ __forceinline__ unsigned long long wgen_sample(WGen& g, uint32_t m, uint32_t n) {
+    if (n == 1u) return 1ull << (wgen_raw(g) % m);
+    const uint32_t l = (uint32_t)lane_id();
+    unsigned long long ch = 0ull;
+    uint32_t need = n, i0 = 0u;
+    for (;;) {
+        wgen_ensure(g);
+        const uint32_t pos = g.pos;
+        const uint32_t avail = 31u - pos, left = m - i0;
+        const uint32_t lim = left < avail ? left : avail;
+        const bool valid = l >= pos && l < pos + lim;
+        // (residues are < m <= 64; a lane outside the window can never be taken)
+        const uint32_t u = valid ? ((g.cur >> 1) & 0x7fffffffu) % (m - (i0 + l - pos)) : 0x40000000u;
+        uint32_t p = pos;  // scan point (lane)
+        // four thresholds per round (need, need - 1, ...): the lanes below each
+        // in one ballot, then the takes are found by scalar ops alone -- the
+        // k-th take of the round is the first lane past the previous take
+        // whose residue is below need - k
+        bool out = false;
+        while (!out) {
+            const uint64_t t0 = __ballot(u < need), t1 = __ballot(u + 1u < need), t2 = __ballot(u + 2u < need),
+                           t3 = __ballot(u + 3u < need);
+            const uint64_t tt[4] = {t0, t1, t2, t3};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint64_t a = tt[q] & (~0ull << p);
+                if (!a) {
+                    p = pos + lim;
+                    out = true;
+                    break;
+                }
+                const uint32_t i = (uint32_t)__ffsll((unsigned long long)a) - 1u;
+                ch |= 1ull << (i0 + i - pos);
+                p = i + 1u;
+                if (--need == 0u) {
+                    out = true;
+                    break;
+                }
+            }
+        }
+        const uint32_t k = p - pos;
+        g.pos = p;
+        g.total += k;
+        i0 += k;
+        if (need == 0u || i0 >= m) return ch;
+    }
+}
+
+// write the generator back to TmSh::rng / rf / rr: slot (f0 + total + j) % 31
+// gets x[n0 + total - 31 + j], the last 31 raw sums (prev[pos..30] then
+// cur[0..pos-1])
+__device__ __forceinline__ void wgen_store(Tm& t, const WGen& g) {
+    TmSh* sh = t.sh;
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t split = 31u - g.pos;
+    const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((g.pos + l) & 63u) << 2), (int)g.prev);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((l + g.pos - 31u) & 63u) << 2), (int)g.cur);
+    const uint32_t x = l < split ? a : b;
+    const uint32_t f1 = (g.f0 + g.total) % 31u;
+    __builtin_amdgcn_wave_barrier();
+    if (l < 31u) {
+        uint32_t fj = f1 + l;
+        fj = fj >= 31u ? fj - 31u : fj;
+        sh->rng[fj] = x;
+    }
+    if (l == 0u) {
+        sh->rf = (int32_t)f1;
+        sh->rr = (int32_t)((f1 + 28u) % 31u);
+    }
+    COUNT(t, SC_LDRAWS, g.total);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 struct WUpd {
     uint32_t mask;   // active existing synapse positions
     uint32_t n_new;  // new sources
@@ -1634,7 +1842,10 @@ __device__ __forceinline__ WUpd w_build_update(Tm& t, uint32_t slot, const uint3
     if (m <= (uint32_t)n) {
         chosen = (m == 64) ? ~0ull : ((1ull << m) - 1ull);
     } else {
+        STAMP(t, SB_LWB);
         chosen = w_rng_sample(t, m, (uint32_t)n);
+        COUNT(t, SC_LSAMPLES, 1);
+        STAMP(t, SB_LWS);
     }
     if (ok && ((chosen >> pos) & 1ull)) {
         uint32_t op = (uint32_t)__popcll(chosen & ((1ull << pos) - 1ull));
@@ -1793,31 +2004,53 @@ __device__ __forceinline__ void w_create_segment(Tm& t, uint32_t cell, uint32_t 
     __builtin_amdgcn_wave_barrier();
 }
 
-// _getCellForNewSegment(colIdx); returns the cell index within the column
-__device__ __forceinline__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
+// the new segment of a wave-parallel learning loop at the slot wave 0 gave it
+// (hwm and the live count were advanced there, in column order)
+__device__ __forceinline__ void w_create_segment_at(Tm& t, uint32_t slot, uint32_t cell, uint32_t n_new,
+                                                    uint32_t my_new) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    if ((uint32_t)l < n_new) {
+        t.src[(size_t)slot * HTM_MAXSYN + l] = (uint16_t)my_new;
+        t.perm[(size_t)slot * HTM_MAXSYN + l] = c.init_perm;
+    }
+    if (l == 0) {
+        uint32_t cm = 0;
+        if (c.init_perm >= c.tm_conn) cm = n_new >= 32 ? 0xFFFFFFFFu : ((1u << n_new) - 1u);
+        t.conn[slot] = cm;
+        t.meta[slot] = make_meta(cell, n_new, 1u, 1u);
+        uint32_t* d = t.duty + (size_t)slot * 3;
+        d[0] = 1u;
+        d[1] = __float_as_uint((float)(1.0 / (double)sh->lrn_iter));
+        d[2] = sh->lrn_iter;
+        atomicAdd(&sh->bytes, (unsigned long long)(4 + 4 + 12 + 6 * n_new + 1));
+        t.nseg[cell] += 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// cells of column col a new segment may go to (getCellForNewSegment's
+// candidates: not cell 0 unless K == 1, fewer than maxSegmentsPerCell
+// segments), bit = cell in column (wave-uniform)
+__device__ __forceinline__ uint32_t w_new_segment_cells(Tm& t, uint32_t col) {
+    const DevCfg& c = t.c;
+    const int l = lane_id();
+    const int K = c.K;
+    const int minIdx = K == 1 ? 0 : 1, maxIdx = K == 1 ? 0 : K - 1;
+    const bool ok = l >= minIdx && l <= maxIdx && (int)t.nseg[col * K + l] < c.max_segs_per_cell;
+    return (uint32_t)__ballot(ok);
+}
+
+// getCellForNewSegment with every cell of the column full: free its
+// least-used segment (smallest refreshed dutyCycle, then lower cell, then
+// slot) and return that cell (minIdx when none qualifies)
+__device__ __forceinline__ uint32_t w_cell_full(Tm& t, uint32_t col) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int l = lane_id();
     const int K = c.K;
-    const int minIdx = K == 1 ? 0 : 1, maxIdx = K == 1 ? 0 : K - 1;
-    bool ok = l >= minIdx && l <= maxIdx && (int)t.nseg[col * K + l] < c.max_segs_per_cell;
-    uint64_t b = __ballot(ok);
-    uint32_t m = (uint32_t)__popcll(b);
-    if (m > 0) {
-        uint32_t idx = 0;
-        if (l == 0) {
-            int32_t f = sh->rf, r = sh->rr;
-            idx = rng_u32(sh->rng, f, r, m);
-            sh->rf = f;
-            sh->rr = r;
-        }
-        idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
-        // position of the idx-th set bit of b
-        uint64_t x = b;
-        for (uint32_t k = 0; k < idx; k++) x &= x - 1ull;
-        return (uint32_t)(__ffsll((unsigned long long)x) - 1);
-    }
-    // all cells full: free the least-used segment of the column
+    const int minIdx = K == 1 ? 0 : 1;
     unsigned long long best = ~0ull;
     const uint32_t hwm = sh->hwm;
     for (uint32_t slot = l; slot < hwm; slot += 64) {
@@ -1849,6 +2082,47 @@ __device__ __forceinline__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) 
     return cic;
 }
 
+// _getCellForNewSegment(colIdx) given its candidate cells b
+// (w_new_segment_cells); returns the cell index within the column
+__device__ __forceinline__ uint32_t w_cell_pick(Tm& t, uint32_t col, uint64_t b) {
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    uint32_t m = (uint32_t)__popcll(b);
+    if (m > 0) {
+        uint32_t idx = 0;
+        if (l == 0) {
+            int32_t f = sh->rf, r = sh->rr;
+            idx = rng_u32(sh->rng, f, r, m);
+            sh->rf = f;
+            sh->rr = r;
+        }
+        idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+        // position of the idx-th set bit of b
+        uint64_t x = b;
+        for (uint32_t k = 0; k < idx; k++) x &= x - 1ull;
+        return (uint32_t)(__ffsll((unsigned long long)x) - 1);
+    }
+    return w_cell_full(t, col);
+}
+
+// the same with the draw from the wave's register generator (draw pass)
+__device__ __forceinline__ uint32_t w_cell_pick(Tm& t, WGen& g, uint32_t col, uint64_t b) {
+    const uint32_t m = (uint32_t)__popcll(b);
+    if (m > 0) {
+        // Random::getUInt32(m): raw draws are < 2^31, so the rejection never fires
+        const uint32_t idx = wgen_raw(g) % m;
+        uint64_t x = b;
+        for (uint32_t k = 0; k < idx; k++) x &= x - 1ull;
+        return (uint32_t)(__ffsll((unsigned long long)x) - 1);
+    }
+    return w_cell_full(t, col);
+}
+
+// _getCellForNewSegment(colIdx); returns the cell index within the column
+__device__ __forceinline__ uint32_t w_cell_for_new_segment(Tm& t, uint32_t col) {
+    return w_cell_pick(t, col, w_new_segment_cells(t, col));
+}
+
 // cells on in `bm` -> sh->cand (<= HTM_MAXACT, ascending)
 __device__ __forceinline__ void build_cand(Tm& t, const uint32_t* bm) {
     uint32_t n = wg_bitmap_list(t, bm, t.sh->cand, nullptr, HTM_MAXACT);
@@ -1857,6 +2131,179 @@ __device__ __forceinline__ void build_cand(Tm& t, const uint32_t* bm) {
         t.sh->ncand = (int32_t)n;
     }
     __syncthreads();
+}
+
+// ---- wave-parallel learning loops (round 5).  A learn phase 1 / 2 loop over
+// columns runs in three barrier-separated passes over one record per column:
+//   build (every wave, columns round-robin): the RNG-free part -- the best
+//       segment's active-synapse mask and the candidates not already on it
+//       (_getSegmentActiveSynapses / _chooseCellsToLearnFrom's filter), or a new
+//       segment's candidate cells (getCellForNewSegment's filter);
+//   draw (wave 0, in NuPIC's column order): only the nupic::Random draws (the new
+//       segment's cell, the sample of new synapses) and the ordered appends (the
+//       new segment's slot at hwm, the queued update's index);
+//   write (every wave): the segment adapt / trim / create, the queued update.
+// Columns touch only their own segments and cells, so only the draws and the
+// appends need the column order; results are those of the serial loop.
+struct __attribute__((aligned(16))) LRec {
+    unsigned long long keep;    // candidates (sh->cand positions) not on the segment
+    unsigned long long chosen;  // bit i: the i-th kept candidate becomes a new synapse
+    uint32_t slot;              // the segment: best match, or the new segment's slot (0xFFFFFFFF: none)
+    uint32_t mask;              // active existing synapses; LR_NEW: the candidate cells of the column
+    uint32_t idx;               // LR_QUEUE: queued-update index (0xFFFFFFFF: not queued)
+    uint16_t col;
+    uint8_t kind;               // LR_ADAPT, LR_NEW, LR_QUEUE
+    uint8_t cic;                // cell in column
+    uint8_t n;                  // new synapses wanted (0: none)
+};
+static_assert(sizeof(LRec) == 48, "LRec: 12 words (LREC_WORDS)");
+enum { LR_ADAPT = 0, LR_NEW = 1, LR_QUEUE = 2 };
+// learning scratch in the union region, past the best-match keys (u64[ncol]):
+// the records, each wave's new-source list, phase 2's key-column list (u16[ncol])
+__device__ __forceinline__ LRec* lrecs(Tm& t) { return reinterpret_cast<LRec*>(t.U + 2 * t.c.ncol); }
+__device__ __forceinline__ uint32_t* lnewsrc(Tm& t) {
+    return t.U + 2 * t.c.ncol + LREC_N * 12 + wave_id() * HTM_MAXSYN;
+}
+__device__ __forceinline__ uint16_t* lkeycols(Tm& t) {
+    return reinterpret_cast<uint16_t*>(t.U + 2 * t.c.ncol + LREC_WORDS);
+}
+
+// build pass of one record: segment `slot` (meta word mw; 0xFFFFFFFF: a new
+// segment) against `state`; the wave's lane 0 stores the record
+__device__ __forceinline__ void w_rec_build(Tm& t, LRec* r, uint32_t kind, uint32_t col, uint32_t cic, uint32_t slot,
+                                            uint32_t mw, const uint32_t* state, bool want_new) {
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    const bool exist = slot != 0xFFFFFFFFu;
+    const uint32_t nsyn = exist ? meta_nsyn(mw) : 0u;
+    const uint32_t mysrc = (exist && (uint32_t)l < nsyn) ? (uint32_t)t.src[(size_t)slot * HTM_MAXSYN + l] : 0xFFFFFFFFu;
+    const bool act = (exist && (uint32_t)l < nsyn) && bm_get(state, mysrc);
+    uint32_t mask = (uint32_t)__ballot(act);
+    if (l == 0 && exist) atomicAdd(&sh->bytes, (unsigned long long)(4 + 2 * nsyn));
+    const int nw = want_new ? t.c.new_syn - __popc(mask) : 0;
+    unsigned long long keep = 0ull;
+    if (nw > 0) {
+        const int ncand = sh->ncand;
+        const uint32_t cv = l < ncand ? sh->cand[l] : 0xFFFFFFFEu;
+        bool ok = l < ncand;
+        for (uint32_t j = 0; j < nsyn; j++) {  // (j uniform: a register read, not an LDS permute)
+            const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)mysrc, (int)j);
+            if (cv == sj) ok = false;
+        }
+        keep = __ballot(ok);
+    }
+    if (kind == LR_NEW) mask = w_new_segment_cells(t, col);
+    if (l == 0) {
+        r->keep = keep;
+        r->chosen = 0ull;
+        r->slot = slot;
+        r->mask = mask;
+        r->idx = 0xFFFFFFFFu;
+        r->col = (uint16_t)col;
+        r->kind = (uint8_t)kind;
+        r->cic = (uint8_t)cic;
+        r->n = (uint8_t)(nw > 0 ? nw : 0);
+    }
+}
+
+// draw pass (wave 0): records [0, nr) in order
+__device__ __forceinline__ void w_rec_draw(Tm& t, LRec* recs, int nr) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    const int l = lane_id();
+    // lane j < nr holds record j's inputs (one LDS round trip for all) and
+    // collects its outputs; the appends' counters stay in scalar registers
+    unsigned long long kk = 0ull;
+    uint32_t kmask = 0u, kcol = 0u, kkn = 0u;
+    if (l < nr) {
+        const LRec& r = recs[l];
+        kk = r.keep;
+        kmask = r.mask;
+        kcol = r.col;
+        kkn = (uint32_t)r.kind | ((uint32_t)r.n << 8);
+    }
+    unsigned long long och = 0ull;
+    uint32_t oslot = 0xFFFFFFFFu, ocic = 0u, oidx = 0xFFFFFFFFu;
+    uint32_t hwm = (uint32_t)__builtin_amdgcn_readfirstlane(sh->hwm);
+    uint32_t nupd = (uint32_t)__builtin_amdgcn_readfirstlane(sh->n_upd);
+    uint32_t nnew = 0u, err = 0u;
+    WGen g = wgen_load(t);
+    for (int j = 0; j < nr; j++) {
+        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)kkn, j);
+        const uint32_t kind = kj & 0xFFu, n = kj >> 8;
+        const unsigned long long keep =
+            (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kk, j) |
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(kk >> 32), j) << 32);
+        const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)kmask, j);
+        uint32_t slot = 0xFFFFFFFFu, cic = 0u;
+        if (kind == LR_NEW) {
+            const uint32_t col = (uint32_t)__builtin_amdgcn_readlane((int)kcol, j);
+            cic = w_cell_pick(t, g, col, (uint64_t)mask);  // (the all-cells-full path reads sh->hwm)
+            if (hwm >= (uint32_t)c.seg_cap) {
+                err |= 1u;
+            } else {
+                slot = hwm++;
+                nnew++;
+                if (l == 0) sh->hwm = hwm;
+            }
+        }
+        const uint32_t m = (uint32_t)__popcll(keep);
+        unsigned long long chosen = 0ull;
+        if (n > 0u && m > 0u) {
+            if (m <= n) {
+                chosen = (m == 64) ? ~0ull : ((1ull << m) - 1ull);
+            } else {
+                chosen = wgen_sample(g, m, n);
+                COUNT(t, SC_LSAMPLES, 1);
+            }
+        }
+        uint32_t idx = 0xFFFFFFFFu;
+        if (kind == LR_QUEUE && (mask != 0u || chosen != 0ull)) {
+            if (nupd >= (uint32_t)c.upd_cap) err |= 2u;
+            else idx = nupd++;
+        }
+        if (l == j) {
+            och = chosen;
+            oslot = slot;
+            ocic = cic;
+            oidx = idx;
+        }
+    }
+    wgen_store(t, g);
+    if (l < nr) {
+        LRec& r = recs[l];
+        r.chosen = och;
+        r.idx = oidx;
+        if ((kkn & 0xFFu) == LR_NEW) {
+            r.slot = oslot;
+            r.cic = (uint8_t)ocic;
+        }
+    }
+    if (l == 0) {
+        sh->hwm = hwm;
+        sh->nlive += nnew;
+        sh->n_upd = (int32_t)nupd;
+        if (err) sh->err |= err;
+    }
+}
+
+// the new sources of a drawn record: lane k (< *n_new) gets the k-th chosen
+// candidate (ascending, as _chooseCellsToLearnFrom lists them)
+__device__ __forceinline__ uint32_t w_rec_sources(Tm& t, unsigned long long keep, unsigned long long chosen,
+                                                  uint32_t* n_new) {
+    const int l = lane_id();
+    uint32_t* ns = lnewsrc(t);
+    const bool kept = l < t.sh->ncand && ((keep >> l) & 1ull);
+    const uint32_t pos = ballot_rank(keep);
+    const bool sel = kept && ((chosen >> pos) & 1ull);
+    const uint64_t sb = __ballot(sel);
+    *n_new = (uint32_t)__popcll(sb);
+    if (sel) ns[ballot_rank(sb)] = t.sh->cand[l];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint32_t v = (uint32_t)l < *n_new ? ns[l] : 0u;
+    __builtin_amdgcn_wave_barrier();  // (the next record's list overwrites ns)
+    return v;
 }
 
 // _processSegmentUpdates(activeColumns)
@@ -1922,6 +2369,8 @@ __device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA
     build_cand(t, t.lrnA1);
     STAMP(t, SB_LEARN);
     const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
+#ifdef HTM_LEARN_SERIAL
+    // (A/B builds: the round-4 loop, wave 0 doing every column in turn)
     if (wave_id() == 0) {
         for (int a = 0; a < nA; a++) {
             uint32_t col = cols[a];
@@ -1934,19 +2383,73 @@ __device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA
                 cic = key_cic(key);
                 seqseg = meta_seq(t.meta[slot]) != 0u;
             }
+            COUNT(t, SC_LP1COLS, 1);
+            STAMP(t, SB_LW);
             if (key && seqseg) {
                 if (lane_id() == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
                 WUpd u = w_build_update(t, slot, t.lrnA1, true);
+                STAMP(t, SB_LWB);
                 bool trim = w_adapt_existing(t, slot, u.mask, u.n_new, u.my_new);
                 if (trim) w_trim_segment(t, slot);
+                STAMP(t, SB_LWW);
             } else {
                 cic = w_cell_for_new_segment(t, col);
+                STAMP(t, SB_LWS);
                 if (lane_id() == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
                 WUpd u = w_build_update(t, 0xFFFFFFFFu, t.lrnA1, true);
+                STAMP(t, SB_LWB);
                 w_create_segment(t, col * K + cic, u.n_new, u.my_new);
+                STAMP(t, SB_LWW);
             }
         }
     }
+#else
+    // the flagged columns in cols order (nA <= 64: one ballot; every wave the same)
+    LRec* recs = lrecs(t);
+    const int l = lane_id();
+    const uint64_t fb =
+        __ballot(l < nA && ((t.flags[cols[l < nA ? l : 0] >> 5] >> (cols[l < nA ? l : 0] & 31)) & 1u));
+    const int nf = __popcll(fb);
+    {
+        uint64_t x = fb;
+        for (int j = 0; x; j++, x &= x - 1ull) {
+            if ((j & (TM_NWAVES - 1)) != wave_id()) continue;
+            const uint32_t col = cols[__ffsll((unsigned long long)x) - 1];
+            const unsigned long long key = keys[col];
+            uint32_t slot = 0xFFFFFFFFu, cic = 0, mw = 0, kind = LR_NEW;
+            if (key) {
+                const uint32_t ks = key_slot(key);
+                mw = t.meta[ks];
+                if (meta_seq(mw)) {
+                    kind = LR_ADAPT;
+                    slot = ks;
+                    cic = key_cic(key);
+                }
+            }
+            w_rec_build(t, &recs[j], kind, col, cic, slot, mw, t.lrnA1, true);
+            COUNT(t, SC_LP1COLS, 1);
+        }
+    }
+    __syncthreads();
+    STAMP(t, SB_LWB);
+    if (wave_id() == 0) w_rec_draw(t, recs, nf);
+    __syncthreads();
+    STAMP(t, SB_LWS);
+    for (int j = wave_id(); j < nf; j += TM_NWAVES) {
+        const LRec& r = recs[j];
+        const uint32_t col = r.col, cic = r.cic, slot = r.slot;
+        uint32_t nn;
+        const uint32_t my_new = w_rec_sources(t, r.keep, r.chosen, &nn);
+        if (l == 0) bm_or_field(t.lrnA, col * K + cic, 1, 1u);
+        if (r.kind == LR_ADAPT) {
+            if (w_adapt_existing(t, slot, r.mask, nn, my_new)) w_trim_segment(t, slot);
+        } else if (slot != 0xFFFFFFFFu) {
+            w_create_segment_at(t, slot, col * K + cic, nn, my_new);
+        }
+    }
+    __syncthreads();
+    STAMP(t, SB_LWW);
+#endif
     __syncthreads();
     STAMP(t, SB_LW);
     return inSeq;
@@ -1974,6 +2477,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
     if (ro) return;
     build_cand(t, t.lrnA);
     STAMP(t, SB_LEARN);
+#ifdef HTM_LEARN_SERIAL
     if (wave_id() == 0) {
         for (int base = 0; base < c.ncol; base += 64) {
             uint64_t b = __ballot(keys[base + lane_id()] != 0ull);
@@ -1983,7 +2487,10 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
                 uint32_t col = (uint32_t)(base + bit);
                 unsigned long long key = keys[col];
                 uint32_t slot = key_slot(key), act = key_act(key);
+                COUNT(t, SC_LP2COLS, 1);
+                STAMP(t, SB_LW);
                 WUpd u = w_build_update(t, slot, t.lrnA, act < (uint32_t)c.new_syn);
+                STAMP(t, SB_LWB);
                 if (u.mask == 0u && u.n_new == 0u) continue;
                 int idx = sh->n_upd;
                 if (idx >= c.upd_cap) {
@@ -2004,9 +2511,64 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
                     atomicAdd(&sh->bytes, (unsigned long long)(2 * (16 + 2 * u.n_new)));
                 }
                 __builtin_amdgcn_wave_barrier();
+                STAMP(t, SB_LWW);
             }
         }
     }
+#else
+    // the columns with a best segment, ascending: thread x lists columns
+    // [x * per, (x + 1) * per)
+    uint16_t* kc = lkeycols(t);
+    const int per = (c.ncol + TM_NT - 1) / TM_NT;
+    const int c0 = threadIdx.x * per;
+    uint32_t cnt = 0;
+    for (int k = 0; k < per; k++)
+        if (c0 + k < c.ncol && keys[c0 + k] != 0ull) cnt++;
+    uint32_t nk;
+    uint32_t pos = wg_excl_scan(sh, cnt, &nk);
+    for (int k = 0; k < per; k++)
+        if (c0 + k < c.ncol && keys[c0 + k] != 0ull) kc[pos++] = (uint16_t)(c0 + k);
+    __syncthreads();
+    LRec* recs = lrecs(t);
+    const int l = lane_id();
+    for (uint32_t b0 = 0; b0 < nk; b0 += LREC_N) {
+        const int nb = nk - b0 < LREC_N ? (int)(nk - b0) : LREC_N;
+        for (int j = wave_id(); j < nb; j += TM_NWAVES) {
+            const uint32_t col = kc[b0 + j];
+            const unsigned long long key = keys[col];
+            const uint32_t slot = key_slot(key);
+            w_rec_build(t, &recs[j], LR_QUEUE, col, key_cic(key), slot, t.meta[slot], t.lrnA,
+                        key_act(key) < (uint32_t)c.new_syn);
+            COUNT(t, SC_LP2COLS, 1);
+        }
+        __syncthreads();
+        STAMP(t, SB_LWB);
+        if (wave_id() == 0) w_rec_draw(t, recs, nb);
+        __syncthreads();
+        STAMP(t, SB_LWS);
+        for (int j = wave_id(); j < nb; j += TM_NWAVES) {
+            const LRec& r = recs[j];
+            const uint32_t idx = r.idx;
+            uint32_t nn;
+            const uint32_t my_new = w_rec_sources(t, r.keep, r.chosen, &nn);
+            if (idx == 0xFFFFFFFFu) continue;
+            htm_tm_update& e = t.upd[idx];
+            if ((uint32_t)l < nn) e.new_src[l] = (uint16_t)my_new;
+            if (l == 0) {
+                e.slot = r.slot;
+                e.col = r.col;
+                e.cell = r.cic;
+                e.n_new = (uint8_t)nn;
+                e.active_mask = r.mask;
+                e.date = sh->lrn_iter;
+                // queued entry written now and read back at the next step
+                atomicAdd(&sh->bytes, (unsigned long long)(2 * (16 + 2 * nn)));
+            }
+        }
+        __syncthreads();
+        STAMP(t, SB_LWW);
+    }
+#endif
     __syncthreads();
     STAMP(t, SB_LW);
 }
@@ -2647,7 +3209,11 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
 // units goes through HBM: agent-scope fences on both sides (the XCDs' L2s
 // are not coherent with each other).
 // SPL = false compiles SP learning out (the frozen bench kernel: inference only)
-template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true>
+#ifndef HTM_SPL_PLANES
+#define HTM_SPL_PLANES 1
+#endif
+// NOSP compiles the SP out (TM-only launches: the SP kernel ran first)
+template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true, bool NOSP = false>
 __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
                                              float* scores, int n_steps, int sp_learn, int keep_prev,
                                              int keep_overlaps, uint32_t* wq, int unit_steps, int n) {
@@ -2716,8 +3282,10 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_STAMPS
         if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (!b.tm_only) {
-            if (SPL && sp_learn) sp_step_body<true, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, bkey, enc, planes);
+        if (!NOSP && !b.tm_only) {
+            if (SPL && sp_learn)
+                sp_step_body<true, PAGED_OK, PAGED_OK || LEARN || HTM_SPL_PLANES>(c, sp, v, s, ssh, keep_overlaps, bkey,
+                                                                                 enc, planes);
             else sp_step_body<false, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
             __syncthreads();
         }
@@ -2780,6 +3348,7 @@ TM_RUN_KERNEL_DECL(run_frozen)
 TM_RUN_KERNEL_DECL(run_frozen_spl)
 TM_RUN_KERNEL_DECL(run_frozen_paged)
 TM_RUN_KERNEL_DECL(run_learn)
+TM_RUN_KERNEL_DECL(run_learn_tm)
 TM_RUN_KERNEL_DECL(run_infer)
 // unfused TM step kernels (learn, frozen index, pool scan)
 int tmk_launch_step(int learn, int frozen, int grid, size_t lds, hipStream_t st, DevCfg c, TmBufs b, SpBufs sp,

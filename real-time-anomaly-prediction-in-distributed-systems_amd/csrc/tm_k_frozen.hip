@@ -14,8 +14,15 @@ __global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_W
     HTM_RUN_ARGS) {
     htm_run_body<false, true, false, false>(HTM_RUN_PASS);
 }
-// TM frozen, SP learning on (ModelTesting's test phase, NetworkModel.py:40-44)
-__global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_RUN_WAVES))) void htm_run_frozen_spl_kernel(
+// TM frozen, SP learning on (ModelTesting's test phase, NetworkModel.py:40-44):
+// the run-mode kernel (lockstep steps of this mode run the SP kernel and then
+// the TM-only launch of htm_run_frozen_kernel).  Two waves per SIMD: at three
+// the SP learning code spilled (168 VGPRs + 20-52 B/lane scratch); at two it
+// takes 193 VGPRs and no scratch
+#ifndef HTM_SPL_WAVES
+#define HTM_SPL_WAVES 2
+#endif
+__global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_SPL_WAVES))) void htm_run_frozen_spl_kernel(
     HTM_RUN_ARGS) {
     htm_run_body<false, true, false, true>(HTM_RUN_PASS);
 }

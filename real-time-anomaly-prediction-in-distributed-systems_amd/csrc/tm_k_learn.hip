@@ -8,11 +8,15 @@
 #ifndef HTM_LEARN_WAVES
 #define HTM_LEARN_WAVES 2
 #endif
+// (A/B probes only: false compiles the paged SP permanences out)
+#ifndef HTM_LEARN_PAGED
+#define HTM_LEARN_PAGED true
+#endif
 
 template <bool LEARN>
 __global__ __launch_bounds__(TM_NT) __attribute__((amdgpu_waves_per_eu(HTM_LEARN_WAVES))) void htm_run_kernel(
     HTM_RUN_ARGS) {
-    htm_run_body<LEARN, false, true>(HTM_RUN_PASS);
+    htm_run_body<LEARN, false, HTM_LEARN_PAGED>(HTM_RUN_PASS);
 }
 
 TM_RUN_KERNEL_EXPORTS(run_learn, htm_run_kernel<true>)

@@ -182,7 +182,7 @@ class HTMEngine:
         """region.getOutputData(...) for every stream (device tensor)."""
         which = OUT[name]
         per = self._L.htm_output_bytes(self.h, which)
-        dtype = {"active_columns": torch.uint8, "prev_pred_columns": torch.uint8,
+        dtype = {"active_columns": torch.uint8, "prev_pred_columns": torch.uint8, "pred_columns": torch.uint8,
                  "col_confidence": torch.float32, "sp_overlaps": torch.int32}.get(name, torch.int32)
         esz = torch.tensor([], dtype=dtype).element_size()
         out = torch.empty((self.n_streams, per // esz), dtype=dtype, device=f"cuda:{self.device}")
@@ -246,6 +246,11 @@ class HTMEngine:
         writes (HTM_OPT_FLUSH_EVERY; 0 = default)."""
         check(self._L.htm_set_option(self.h, _lib.OPT_FLUSH_EVERY, int(steps)))
 
+    def split_learning(self, on: bool):
+        """Learning lockstep steps run the SP kernel, then the TM-only learning
+        kernel (HTM_OPT_SPLIT_LEARN, default on); results are identical."""
+        check(self._L.htm_set_option(self.h, _lib.OPT_SPLIT_LEARN, int(on)))
+
     def ordered_steps(self, on: bool):
         """Frozen lockstep steps run their TM steps heaviest first
         (HTM_OPT_ORDERED, default on); results are identical either way."""
@@ -295,10 +300,12 @@ class HTMEngine:
         check(self._L.htm_debug_stamps(self.h, out))
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
                  "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp", "norm",
-                 "learn_scan", "learn_updates", "learn_wave0", "learn_bt_copy", "compact", "sp_learn"]
+                 "learn_scan", "learn_updates", "learn_wave0", "learn_bt_copy", "compact", "sp_learn",
+                 "lw_build", "lw_draws", "lw_writes"]
         cnames = {0: "phase2", 1: "windows", 2: "blocks", 3: "qualifying", 4: "active_cells", 5: "nonzero_cols",
                   6: "steps", 16: "pool_scans", 17: "pool_scan_slots", 18: "sp_row_replays",
-                  19: "sp_row_replay_cycles", 20: "sp_row_replay_sample_cycles", 21: "sp_row_replay_skip_cycles"}
+                  19: "sp_row_replay_cycles", 20: "sp_row_replay_sample_cycles", 21: "sp_row_replay_skip_cycles",
+                  22: "lp1_columns", 23: "lp2_columns", 24: "lw_samples", 25: "lw_sample_draws"}
 
         def part(o):
             return dict(cycles={k: int(out[o + i]) for i, k in enumerate(names)},

@@ -7,7 +7,8 @@ Config 3: 65,536 streams learning on (BASELINE configs[2]) with the paged SP
           permanences the bench uses (htm_config.sp_perm_rows): 512 fresh
           streams with per-stream seeds, every step of 8 sampled streams
           checked against the oracle and the full SP/TM state of two; and the
-          full 65,536 streams, 5 sampled streams against the oracle.
+          full 65,536 streams over config 3's 256 steps, 5 sampled streams
+          against the oracle every step.
 Config 4: fleet mode, 131,072 streams sharing one frozen model (configs[3]).
 Config 5: the cpu / mem / mean / max response-time aggregate
           (StreamEngine/StreamAggregator.py:101-115) through a 4-field
@@ -184,26 +185,37 @@ def test_config3_many_fresh_streams_learning(rt, oracle_mod):
 
 
 def test_config3_65536_streams_paged_vs_oracle(rt, oracle_mod, traces):
-    """Config 3 at its stated size: 65,536 fresh learning streams (seed 2045 + s)
-    on one GPU with paged SP permanences, the bench's inputs (trace + jitter),
-    32 lockstep steps; 5 sampled streams equal independent oracle models at
-    every step, one of them in its whole SP state."""
+    """Config 3 at its stated size and horizon (65,536 fresh
+    learning streams, T = 256; the reference trains through the whole file,
+    ModelTraining.py:91-93): seed 2045 + s, one GPU, paged SP permanences, the
+    bench's inputs (trace + jitter), 256 lockstep steps; 5 sampled streams
+    equal independent oracle models at every step -- score, SP active columns
+    and TM output cells -- and, after the last step, one in its whole SP state
+    and one in its whole TM state (segments, synapses, permanences, RNG)."""
     import bench
-    n, T = 65536, 32
+    n, T = 65536, 256
+    sampled = (0, 1, 31337, 40961, n - 1)
     trace = np.asarray(traces["test"], np.float64)
     vals = bench.make_inputs(n, 0, n, 0, T, trace)
     cfg = rt.default_config(seg_capacity=10240, upd_capacity=512, seed_stride=1, sp_perm_rows=800)
     eng = rt.HTMEngine(n, config=cfg)
     v = torch.tensor(vals, device="cuda")
-    got = np.stack([eng.step(v[k]).cpu().numpy() for k in range(T)])
+    idx = torch.tensor(sampled, device="cuda")
+    orcs = [oracle_mod.OracleModel(sp_seed=2045 + s, tm_seed=2045 + s) for s in sampled]
+    for k in range(T):
+        got = eng.step(v[k]).index_select(0, idx).cpu().numpy()
+        act = eng.get_output("active_columns").index_select(0, idx).cpu().numpy()
+        out = eng.bitmap_to_dense(eng.get_output("tm_output").index_select(0, idx))
+        for i, (s, o) in enumerate(zip(sampled, orcs)):
+            assert got[i] == o.step([vals[k, s]], True, True), f"step {k} stream {s}: score"
+            ao = np.zeros(eng.n_columns, np.uint8)
+            ao[o.active_columns()] = 1
+            assert np.array_equal(act[i], ao), f"step {k} stream {s}: active columns"
+            assert np.array_equal(out[i], o.tm_output()), f"step {k} stream {s}: TM output cells"
     eng.status()
     assert 0 < eng.sp_perm_rows_used() <= n * 800
-    for s in (0, 1, 31337, 40961, n - 1):
-        o = oracle_mod.OracleModel(sp_seed=2045 + s, tm_seed=2045 + s)
-        want = np.array([o.step([vals[k, s]], True, True) for k in range(T)], np.float32)
-        assert np.array_equal(got[:, s], want), f"stream {s}"
-        if s == n - 1:
-            sp_equal(eng, s, o)
+    sp_equal(eng, n - 1, orcs[-1])
+    tm_equal(eng, 31337, orcs[2])
 
 
 # response times in ms next to cpu/mem percent: per-field encoder ranges

@@ -9,7 +9,9 @@ as one htm_run chunk, then lockstep htm_step with the deferred dutyCycle()
 writes on (HTM_OPT_DEFER_DUTY, flushed beside the steps on the engine's own
 stream).  Sampled streams -- including both sides of the 768-workgroup
 residency boundary (3 per CU x 256 CUs) and the last stream -- are held
-against independent oracle clones on every step; after htm_flush the full TM
+against independent oracle clones on every step: the score, the SP active
+columns, the TM output cells and the predicted-column set (nonzero
+colConfidence) of each step; after htm_flush the full TM
 state of two streams (segment dutyCycle records included) must equal the
 oracle's.  Oracle parity w.r.t. NuPIC itself is unpinned.
 
@@ -49,14 +51,25 @@ def test_config2_lockstep_1024_replicas_vs_oracle(rt, oracle_mod, traces):
         for k in range(warm):
             assert g[k, s] == o.step([host[k, s]], False, False), f"warm-up step {k} stream {s}"
     c0 = eng.counters()
+    idx = torch.tensor(SAMPLED, device="cuda")
     for k in range(warm, warm + T):
         eng.step(vals[k], out=scores[k])  # bench's timed region: lockstep
-        if (k - warm) % 16 == 15:
-            got = scores[k - 15:k + 1].cpu().numpy()
-            for s, o in orcs.items():
-                for j in range(16):
-                    kk = k - 15 + j
-                    assert got[j, s] == o.step([host[kk, s]], False, False), f"lockstep step {kk} stream {s}"
+        # the SDR state of every sampled stream at this step (north_star: bit-exact
+        # SDR state per step): SP active columns, TMRegion bottomUpOut (infActive |
+        # infPredicted cells) and the predicted-column set nonzero(colConfidence(t))
+        # the next score reads -- read without touching the packed state
+        act = eng.get_output("active_columns").index_select(0, idx).cpu().numpy()
+        out = eng.bitmap_to_dense(eng.get_output("tm_output").index_select(0, idx))
+        pred = eng.get_output("pred_columns").index_select(0, idx).cpu().numpy()
+        got = scores[k].cpu().numpy()
+        for i, (s, o) in enumerate(orcs.items()):
+            assert got[s] == o.step([host[k, s]], False, False), f"lockstep step {k} stream {s}: score"
+            ao = np.zeros(eng.n_columns, np.uint8)
+            ao[o.active_columns()] = 1
+            assert np.array_equal(act[i], ao), f"lockstep step {k} stream {s}: active columns"
+            assert np.array_equal(out[i], o.tm_output()), f"lockstep step {k} stream {s}: TM output cells"
+            po = (o.col_confidence() != 0).astype(np.uint8)
+            assert np.array_equal(pred[i], po), f"lockstep step {k} stream {s}: predicted columns"
     eng.flush()
     c1 = eng.counters()
     assert c1["error"] == 0

@@ -8,6 +8,7 @@ command (tools/gpu_prof.sh):
   pmc_fetch/  FETCH_SIZE
   pmc_wr/     WRITE_SIZE TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
   pmc_l2/     TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum (optional: fleets, whose shared model is L2-served)
+  pmc_sq1/, pmc_sq2/  SQ counters (optional): issue / wait fractions of the waves' cycles
   prof/       --kernel-trace --stats (kernel_stats.csv is copied along)
 Counters are per dispatch; the median over the dispatches of each kernel is
 reported.  Read bytes are counted from the L2 memory-side read requests by
@@ -47,11 +48,69 @@ def med(d, k, c):
     return statistics.median(v) if v else None
 
 
+# SQ passes (8 SQ counters each): where the waves' cycles go.  SQ_WAVE_CYCLES,
+# SQ_WAIT_* and SQ_ACTIVE_INST_* count quad-cycles summed over waves;
+# WAIT_ANY (parked on s_waitcnt / s_barrier) + WAIT_INST_ANY (ready, not
+# issued) + ACTIVE_INST_ANY (issuing) ~= WAVE_CYCLES (MI355X_MICROARCH.md,
+# rocprofv3 PMC slots).
+SQ_PASSES = ("pmc_sq1", "pmc_sq2", "pmc_sq3")
+
+
+def sq_summary(sq, k):
+    """Fractions of the waves' cycles (median per dispatch) from the SQ passes;
+    each counter is divided by SQ_WAVE_CYCLES of its own pass (every SQ pass
+    collects it)."""
+    def g(c):
+        for d in sq:
+            v = med(d, k, c)
+            if v is not None:
+                return v
+        return None
+
+    def frac(c):
+        for d in sq:
+            v, w = med(d, k, c), med(d, k, "SQ_WAVE_CYCLES")
+            if v is not None and w:
+                return round(v / w, 4)
+        return None
+    wc = g("SQ_WAVE_CYCLES")
+    if not wc:
+        return None
+    out = {"waves": g("SQ_WAVES"), "wave_cycles": wc, "busy_cycles": g("SQ_BUSY_CYCLES")}
+    for name, c in (("issue_active", "SQ_ACTIVE_INST_ANY"), ("waiting", "SQ_WAIT_ANY"),
+                    ("issue_stalled", "SQ_WAIT_INST_ANY"), ("valu", "SQ_ACTIVE_INST_VALU"),
+                    ("salu", "SQ_ACTIVE_INST_SCA"), ("lds", "SQ_ACTIVE_INST_LDS"),
+                    ("vmem", "SQ_ACTIVE_INST_VMEM"), ("flat", "SQ_ACTIVE_INST_FLAT"),
+                    ("misc", "SQ_ACTIVE_INST_MISC"), ("lds_issue_stalled", "SQ_WAIT_INST_LDS")):
+        v = frac(c)
+        if v is not None:
+            out[name] = v
+    bc, la = g("SQ_LDS_BANK_CONFLICT"), g("SQ_LDS_IDX_ACTIVE")
+    if bc is not None and la:
+        out["lds_bank_conflict_over_lds_active"] = round(bc / la, 4)
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_INSTS_SMEM", "SQ_INSTS_FLAT",
+              "SQ_INSTS_BRANCH", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INST_LEVEL_VMEM",
+              "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+        v = g(c)
+        if v is not None:
+            out.setdefault("counts", {})[c] = v
+    if out.get("waves"):
+        out["cycles_per_wave"] = round(4 * wc / out["waves"], 1)  # quad-cycles -> shader cycles
+    out["note"] = ("fractions of SQ_WAVE_CYCLES (median per dispatch): issue_active = ACTIVE_INST_ANY, "
+                   "waiting = WAIT_ANY (s_waitcnt on memory/LDS or s_barrier), issue_stalled = WAIT_INST_ANY; "
+                   "per-unit issue fractions (valu, salu, lds, vmem, flat) overlap")
+    return out
+
+
 def summarise(run):
     rd, fe, wr, l2 = (load_pass(os.path.join(run, p)) for p in ("pmc_rd", "pmc_fetch", "pmc_wr", "pmc_l2"))
+    sq = [load_pass(os.path.join(run, p)) for p in SQ_PASSES]
     kernels = {}
-    for k in set(rd) | set(fe) | set(wr) | set(l2):
+    for k in set(rd) | set(fe) | set(wr) | set(l2) | set().union(*sq):
         e = {}
+        sqs = sq_summary(sq, k)
+        if sqs:
+            e["sq"] = sqs
         hit, miss, req = (med(l2, k, c) for c in ("TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum"))
         if None not in (hit, miss):
             e["l2"] = {"hit": hit, "miss": miss, "req": req,
@@ -71,7 +130,7 @@ def summarise(run):
         if ws is not None:
             e["write_size_bytes"] = ws * 1024
         n = max(len(d.get(k, {}).get(c, [])) for d, c in ((rd, "TCC_EA0_RDREQ_sum"), (fe, "FETCH_SIZE"),
-                                                         (wr, "WRITE_SIZE")))
+                                                         (wr, "WRITE_SIZE"), *((x, "SQ_WAVE_CYCLES") for x in sq)))
         e["dispatches"] = n
         if "read_bytes" in e and "write_bytes" in e:
             e["hbm_bytes_per_dispatch"] = e["read_bytes"] + e["write_bytes"]

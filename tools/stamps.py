@@ -45,6 +45,7 @@ st = eng.debug_stamps()
 steps = st["counts"]["steps"]
 tot = sum(st["cycles"].values())
 out = {"mode": MODE, "streams": N, "steps": T, "warmup": W, "tm_ms_per_launch": prof["tm_ms"] / prof["steps"],
+       "sp_ms_per_launch": prof["sp_ms"] / prof["steps"],
        "cycles_per_stream_step": {k: round(v / steps, 1) for k, v in st["cycles"].items()},
        "total_cycles_per_stream_step": round(tot / steps, 1),
        "counts_per_stream_step": {k: round(v / steps, 3) for k, v in st["counts"].items()},
