@@ -398,6 +398,57 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return lane63(v);
 }
 
+// v with lane `lane` replaced by the wave-uniform x (v_writelane_b32: no
+// per-lane mask; clang has no builtin for it)
+template <int LANE>
+__device__ __forceinline__ uint32_t writelane_u32(uint32_t v, uint32_t x) {
+    const uint32_t xs = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(xs), "i"(LANE));
+    return v;
+}
+
+// nupic::Random's next block of 31 raw sums across the lanes: lane j < 31
+// holds v[j] = x[n-31+j] of the window and gets y[j] = x[n+j] = v[j] +
+// (j >= 3 ? y[j-3] : v[28+j]) (TM learning's draw pass, the SP's paged-row
+// replay).  Lanes 0..2 get their base v[28 + j] added, then an inclusive scan
+// over stride 3 inside each 16-lane row (DPP row_shr 3, 6, 12: residue
+// classes never mix), and row 0's per-residue totals (lanes 15, 13, 14) are
+// carried into row 1 by a second such scan.  No LDS round trip, no per-lane
+// masks.  Call with every lane of the wave.
+__device__ __forceinline__ uint32_t rng_block_lanes(uint32_t v) {
+    // lanes 0..2 start from v[j] + v[28 + j] (the recurrence's base), so the
+    // stride-3 scan carries it into every later lane of the residue; no
+    // per-residue lane masks (as loop-invariant SGPR masks they were spilled)
+    uint32_t p = v;
+    p = writelane_u32<0>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 28));
+    p = writelane_u32<1>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 1) + (uint32_t)__builtin_amdgcn_readlane((int)v, 29));
+    p = writelane_u32<2>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 2) + (uint32_t)__builtin_amdgcn_readlane((int)v, 30));
+    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x113, 0xF, 0xF, false);  // row_shr:3
+    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x116, 0xF, 0xF, false);  // row_shr:6
+    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x11C, 0xF, 0xF, false);  // row_shr:12
+    // row 0's totals per residue (lanes 15, 13, 14) enter row 1 at its first
+    // lane of that residue (18, 16, 17) and are carried by the same scan
+    uint32_t q = 0u;
+    q = writelane_u32<16>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 13));
+    q = writelane_u32<17>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 14));
+    q = writelane_u32<18>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 15));
+    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x113, 0xF, 0xF, false);
+    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x116, 0xF, 0xF, false);
+    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x11C, 0xF, 0xF, false);
+    return p + q;
+}
+
+// OR over the wave (all 64 lanes active): a DPP scan read from lane 63
+__device__ __forceinline__ uint32_t wave_or_dpp(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return lane63(v);
+}
+
 // number of set bits of a 64-bit ballot below this lane
 __device__ __forceinline__ uint32_t ballot_rank(uint64_t ball) {
     uint64_t m = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));

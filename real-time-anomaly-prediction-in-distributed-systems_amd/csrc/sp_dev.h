@@ -586,18 +586,8 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
         uint32_t v = 0;
 #pragma unroll
         for (int j = 0; j < 31; j++) v = l == (uint32_t)j ? st[(3 + j) % 31] : v;
-        const uint32_t m3 = l % 3u;
         while (i < npd) {
-            uint32_t p = v;
-#pragma unroll
-            for (int d = 3; d < 31; d *= 2) {
-                const uint32_t up = (uint32_t)__shfl_up((int)p, d, 64);
-                if (l >= (uint32_t)d) p += up;
-            }
-            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 28);
-            const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 29);
-            const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 30);
-            v = p + (m3 == 0u ? b0 : m3 == 1u ? b1 : b2);  // the next window = this block's values
+            v = rng_block_lanes(v);  // the next window = this block's values (DPP, htm_dev.h)
             // block draw j (lanes < 31): skipped while j < sk, else column draw i + j - sk
             if (l < 31u && l >= sk && i + (l - sk) < npd) lb[(i + (l - sk)) & 511u] = (v >> 1) & 0x7fffffffu;
             i += 31u - sk;

@@ -125,8 +125,9 @@ enum { SC_P2 = 0, SC_WIN, SC_BLK, SC_QN, SC_NACT, SC_TNZ, SC_STEPS, SC_HIST };
 // the slots they swept, SP paged-row replays and the lane-0 cycles they took
 // (summed over waves; filled in by htm_debug_stamps from SpBufs::dbg)
 enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC, SC_REPLAYSAMPLE, SC_REPLAYSKIP,
-       // learning loops: columns of learn phase 1 / 2, sampling calls, draws consumed
-       SC_LP1COLS, SC_LP2COLS, SC_LSAMPLES, SC_LDRAWS };
+       // learning loops: columns of learn phase 1 / 2, sampling calls, draws consumed,
+       // the cycles inside the samples, generator blocks made
+       SC_LP1COLS, SC_LP2COLS, SC_LSAMPLES, SC_LDRAWS, SC_LSAMPLECYC, SC_LBLOCKS };
 
 // learning loops (wave-parallel, round 5): column records per pass (learn
 // phase 1: <= HTM_MAXACT columns; phase 2 in batches) and their LDS words
@@ -418,18 +419,22 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
                 // trip; a per-synapse `j < nsyn &&` test made a branch and a
                 // wait per read), entries past nsyn clamped into the bitmap and
                 // masked off afterwards
-                uint32_t bits = 0;
+                uint32_t sw[8];
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    const uint32_t sid = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-                    const uint32_t wi = sid >> 5;
-                    bits |= ((state[wi < cwm1 ? wi : cwm1] >> (sid & 31)) & 1u) << k;
+                    const uint32_t wi = (w[k >> 1] >> ((k & 1) * 16 + 5)) & 0x7FFu;
+                    sw[k] = state[wi < cwm1 ? wi : cwm1];
                 }
+                uint32_t bits = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) bits |= ((sw[k] >> ((w[k >> 1] >> ((k & 1) * 16)) & 31u)) & 1u) << k;
                 const uint32_t left = nsyn - sub * 8u;
                 mask = (bits & (left >= 8u ? 0xFFu : (1u << left) - 1u)) << (sub * 8u);
             }
-            mask |= __shfl_xor(mask, 1, 64);
-            mask |= __shfl_xor(mask, 2, 64);
+            // OR over the segment's four lanes: DPP quad permutes (a __shfl_xor
+            // is a ds_bpermute, an LDS round trip)
+            mask |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mask, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+            mask |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mask, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
             f(slot, m[d], el[d], mask);
         }
     }
@@ -1660,38 +1665,6 @@ struct WGen {
     uint32_t f0;         // the loaded state's front pointer (uniform)
 };
 
-// v with lane `lane` replaced by the wave-uniform x (v_writelane_b32: no
-// per-lane mask; clang has no builtin for it)
-template <int LANE>
-__device__ __forceinline__ uint32_t writelane_u32(uint32_t v, uint32_t x) {
-    const uint32_t xs = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
-    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(xs), "i"(LANE));
-    return v;
-}
-
-__device__ __forceinline__ uint32_t wgen_block(uint32_t v) {
-    // lanes 0..2 start from v[j] + v[28 + j] (the recurrence's base), so the
-    // stride-3 scan carries it into every later lane of the residue; no
-    // per-residue lane masks (as loop-invariant SGPR masks they were spilled)
-    uint32_t p = v;
-    p = writelane_u32<0>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 28));
-    p = writelane_u32<1>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 1) + (uint32_t)__builtin_amdgcn_readlane((int)v, 29));
-    p = writelane_u32<2>(p, (uint32_t)__builtin_amdgcn_readlane((int)v, 2) + (uint32_t)__builtin_amdgcn_readlane((int)v, 30));
-    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x113, 0xF, 0xF, false);  // row_shr:3
-    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x116, 0xF, 0xF, false);  // row_shr:6
-    p += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p, 0x11C, 0xF, 0xF, false);  // row_shr:12
-    // row 0's totals per residue (lanes 15, 13, 14) enter row 1 at its first
-    // lane of that residue (18, 16, 17) and are carried by the same scan
-    uint32_t q = 0u;
-    q = writelane_u32<16>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 13));
-    q = writelane_u32<17>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 14));
-    q = writelane_u32<18>(q, (uint32_t)__builtin_amdgcn_readlane((int)p, 15));
-    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x113, 0xF, 0xF, false);
-    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x116, 0xF, 0xF, false);
-    q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x11C, 0xF, 0xF, false);
-    return p + q;
-}
-
 __device__ __forceinline__ WGen wgen_load(Tm& t) {
     TmSh* sh = t.sh;
     const uint32_t l = (uint32_t)lane_id();
@@ -1709,7 +1682,7 @@ __device__ __forceinline__ WGen wgen_load(Tm& t) {
 __device__ __forceinline__ void wgen_ensure(WGen& g) {
     if (g.pos == 31u) {
         g.prev = g.cur;
-        g.cur = wgen_block(g.prev);
+        g.cur = rng_block_lanes(g.prev);
         g.pos = 0u;
     }
 }
@@ -1747,12 +1720,13 @@ __device__ __forceinline__ unsigned long long wgen_sample(WGen& g, uint32_t m, u
         // four thresholds per round (need, need - 1, ...): the lanes below each
         // in one ballot, then the takes are found by scalar ops alone -- the
         // k-th take of the round is the first lane past the previous take
-        // whose residue is below need - k
+        // whose residue is below need - k; the block's taken lanes are kept as
+        // a lane mask and moved into candidate order once per block
+        uint64_t taken = 0ull;
         bool out = false;
         while (!out) {
-            const uint64_t t0 = __ballot(u < need), t1 = __ballot(u + 1u < need), t2 = __ballot(u + 2u < need),
-                           t3 = __ballot(u + 3u < need);
-            const uint64_t tt[4] = {t0, t1, t2, t3};
+            const uint64_t tt[4] = {__ballot(u < need), __ballot(u + 1u < need), __ballot(u + 2u < need),
+                                    __ballot(u + 3u < need)};
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const uint64_t a = tt[q] & (~0ull << p);
@@ -1762,7 +1736,7 @@ __device__ __forceinline__ unsigned long long wgen_sample(WGen& g, uint32_t m, u
                     break;
                 }
                 const uint32_t i = (uint32_t)__ffsll((unsigned long long)a) - 1u;
-                ch |= 1ull << (i0 + i - pos);
+                taken |= 1ull << i;
                 p = i + 1u;
                 if (--need == 0u) {
                     out = true;
@@ -1770,6 +1744,7 @@ __device__ __forceinline__ unsigned long long wgen_sample(WGen& g, uint32_t m, u
                 }
             }
         }
+        ch |= (taken >> pos) << i0;
         const uint32_t k = p - pos;
         g.pos = p;
         g.total += k;
@@ -1800,6 +1775,7 @@ __device__ __forceinline__ void wgen_store(Tm& t, const WGen& g) {
         sh->rr = (int32_t)((f1 + 28u) % 31u);
     }
     COUNT(t, SC_LDRAWS, g.total);
+    COUNT(t, SC_LBLOCKS, (g.total + 30u) / 31u);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
@@ -1858,11 +1834,7 @@ __device__ __forceinline__ WUpd w_build_update(Tm& t, uint32_t slot, const uint3
     return u;
 }
 
-__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) { return wave_or_dpp(v); }
 
 // _adaptSegment on an existing segment; returns trimSegment (wave-uniform)
 __device__ __forceinline__ bool w_adapt_existing(Tm& t, uint32_t slot, uint32_t amask, uint32_t n_new, uint32_t my_new) {
@@ -2253,8 +2225,14 @@ __device__ __forceinline__ void w_rec_draw(Tm& t, LRec* recs, int nr) {
             if (m <= n) {
                 chosen = (m == 64) ? ~0ull : ((1ull << m) - 1ull);
             } else {
+#ifdef HTM_STAMPS
+                const uint64_t ts0_ = __builtin_amdgcn_s_memtime();
+#endif
                 chosen = wgen_sample(g, m, n);
                 COUNT(t, SC_LSAMPLES, 1);
+#ifdef HTM_STAMPS
+                COUNT(t, SC_LSAMPLECYC, __builtin_amdgcn_s_memtime() - ts0_);
+#endif
             }
         }
         uint32_t idx = 0xFFFFFFFFu;

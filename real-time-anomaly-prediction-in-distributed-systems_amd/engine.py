@@ -305,7 +305,8 @@ class HTMEngine:
         cnames = {0: "phase2", 1: "windows", 2: "blocks", 3: "qualifying", 4: "active_cells", 5: "nonzero_cols",
                   6: "steps", 16: "pool_scans", 17: "pool_scan_slots", 18: "sp_row_replays",
                   19: "sp_row_replay_cycles", 20: "sp_row_replay_sample_cycles", 21: "sp_row_replay_skip_cycles",
-                  22: "lp1_columns", 23: "lp2_columns", 24: "lw_samples", 25: "lw_sample_draws"}
+                  22: "lp1_columns", 23: "lp2_columns", 24: "lw_samples", 25: "lw_sample_draws",
+                  26: "lw_sample_cycles", 27: "lw_blocks_approx"}
 
         def part(o):
             return dict(cycles={k: int(out[o + i]) for i, k in enumerate(names)},
