@@ -512,9 +512,12 @@ def main():
                          "reference's test phase, NetworkModel.py:40-44)")
     ap.add_argument("--test-phase-steps", type=int, default=256, help="test_phase: timed lockstep steps")
     ap.add_argument("--test-phase-warmup", type=int, default=16, help="test_phase: untimed steps")
-    ap.add_argument("--flush-mode", choices=["auto", "0", "1"], default="auto",
+    ap.add_argument("--flush-mode", choices=["auto", "0", "1", "2"], default="auto",
                     help="where the deferred-write flush runs (HTM_OPT_FLUSH_MODE): 0 beside the steps on the "
                          "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
+    ap.add_argument("--wide", type=int, default=0,
+                    help="HTM_OPT_WIDE: up to N of an ordered launch's heaviest TM steps by 768-thread workgroups "
+                         "beside the 256-thread launch (0: off); results identical")
     ap.add_argument("--ordered", choices=["on", "off"], default="on",
                     help="HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first (on, the engine "
                          "default) or one fused SP+TM workgroup per stream in stream order (off); results identical")
@@ -634,6 +637,8 @@ def main():
         eng.set_run_unit(args.run_unit)
     if args.ordered == "off" and not standin:
         eng.ordered_steps(False)
+    if args.wide and not standin:
+        eng.wide_steps(args.wide)
     C = args.condition
     # the reference's test phase (SP learning on, TM learning off) on the same
     # engine after the headline and run-mode regions: config 2, Model-1 shape
@@ -769,7 +774,7 @@ def main():
                                if ordered else "")
                             if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
-                   "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered,
+                   "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered, "wide": args.wide,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
                    "cells_per_column": eng.cells_per_column,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
@@ -859,6 +864,8 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
             child += ["--flush-mode", args.flush_mode]
         if args.ordered != "on":
             child += ["--ordered", args.ordered]
+        if args.wide:
+            child += ["--wide", str(args.wide)]
         for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows", "condition"):
             v = getattr(args, k)
             if v is not None:

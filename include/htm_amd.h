@@ -193,6 +193,9 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    learning included) and then the TM learning kernel with the SP compiled out
                                    (each at its own occupancy); results are identical.  0: one fused SP+TM
                                    learning kernel */
+#define HTM_OPT_WIDE 15         /* ordered frozen lockstep steps: 0 (default) every TM step by a 256-thread
+                                   workgroup; N > 0: up to N of the heaviest steps (the top cost buckets)
+                                   by 768-thread workgroups in a launch beside the others; results identical */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued

@@ -2817,6 +2817,125 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     if (threadIdx.x == 0) t.sh->acc[0] = t.sh->acc[1] = t.sh->acc[2] = 0u;  // (a barrier follows before any use)
 }
 
+// Replay one deferred-log entry of stream s (ring slot i, `len` cells): its
+// active cells, the counting of rank window `win` (-1: every window), the
+// qualifying segments' first dutyCycle() record writes (phase2_duty_only).
+// The calling workgroup's qualifying list is fx_fq's row `worker`.  Used by
+// tm_fx_flush_kernel and by the tail workers of ordered launches.
+__device__ __forceinline__ void fx_replay_entry(const DevCfg& c, const TmBufs& b, int s, uint32_t i, uint32_t len,
+                                                int win, uint32_t worker, uint8_t* lds) {
+    Tm t;
+    tm_bind<false, true>(t, c, b, s, s, lds);
+    t.q1 = b.fx_fq + (size_t)worker * c.q_cap;
+    t.defer = false;
+    TmSh* sh = t.sh;
+    if (threadIdx.x == 0) {
+        sh->qn = 0;
+        sh->bytes = 0;
+        sh->lrn_iter = b.hdr[s].lrn_iter;  // frozen while TM learning is off
+        sh->p1_n = -1;                      // infA comes from the log, not from a phase 1
+    }
+    wg_clear(t.infA, c.cw);
+    __syncthreads();
+    const uint16_t* cl = b.fx_dlog + ((size_t)s * (uint32_t)c.fx_dcap + i) * fx_dstride(c);
+    for (uint32_t k = threadIdx.x; k < len; k += TM_NT) {
+        const uint32_t cell = cl[k];
+        if (cell < (uint32_t)c.ncells) atomicOr(&t.infA[cell >> 5], 1u << (cell & 31));
+    }
+    __syncthreads();
+    collect_frozen(t, c.act_thr, FX_WIN, win);
+    __syncthreads();
+    if (threadIdx.x == 0 && (uint32_t)sh->qn > (uint32_t)c.q_cap) {
+        atomicOr(&b.fx_fwork[1], FX_ERR_QCAP);  // qualifying-list overflow, as in the step (htm_status)
+        sh->qn = c.q_cap;
+    }
+    __syncthreads();
+    phase2_duty_only(t);
+}
+
+// A tail worker of an ordered frozen launch (TmBufs::fx_tjob): claims the
+// jobs the previous tail launch's steps published -- one per stream, the
+// entries [first, end) of its ring -- replays them, and marks them flushed
+// (fx_dflushed only grows: atomicMax).  The workers start once every stream
+// workgroup is dispatched, so they fill the slots the draining steps free.
+// Worker 0 first clears the buffer the next launch publishes into.
+__device__ __forceinline__ void fx_tail_worker(const DevCfg& c, const TmBufs& b, int n, uint8_t* lds) {
+    __shared__ uint32_t job_sh;
+    const uint32_t worker = blockIdx.x - (uint32_t)n;
+    const uint32_t par = b.fx_tpar, rd = (par + 2u) % 3u, nx = (par + 1u) % 3u;
+    const uint32_t dcap = (uint32_t)c.fx_dcap;
+    if (worker == 0 && threadIdx.x == 0) {
+        b.fx_fwork[FX_TCNT + nx] = 0u;
+        b.fx_fwork[FX_TCLAIM + nx] = 0u;
+    }
+    uint32_t total = b.fx_fwork[FX_TCNT + rd];
+    total = total < (uint32_t)c.n_streams ? total : (uint32_t)c.n_streams;
+    const uint4* jobs = b.fx_tjob + (size_t)rd * (uint32_t)c.n_streams;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) job_sh = atomicAdd(&b.fx_fwork[FX_TCLAIM + rd], 1u);
+        __syncthreads();
+        const uint32_t j = __builtin_amdgcn_readfirstlane(job_sh);
+        if (j >= total) break;
+        const uint4 jb = jobs[j];
+        const uint32_t su = __builtin_amdgcn_readfirstlane(jb.x), f = __builtin_amdgcn_readfirstlane(jb.y),
+                       u = __builtin_amdgcn_readfirstlane(jb.z);
+        if (su >= (uint32_t)n || u - f > dcap) {
+            if (threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOB);
+            continue;
+        }
+        for (uint32_t e = f; e != u; e++) {
+            const uint32_t i = e % dcap;
+            const uint32_t len = b.fx_dlen[(size_t)su * dcap + i];
+            if (len > (uint32_t)c.max_act_cells) {
+                if (threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOB);
+                continue;
+            }
+            fx_replay_entry(c, b, (int)su, i, len, -1, worker, lds);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&b.fx_dflushed[su], u);
+    }
+}
+
+// Stream of wide workgroup b (HTM_OPT_WIDE): the b-th stream, in stream
+// order, whose cost bucket is >= wide_q, if b < wide_max; else -1 -- the same
+// streams ord_sort_kernel leaves out of the 256-thread launch's list.  Every
+// thread returns it.  Contains barriers: call uniformly.
+__device__ __forceinline__ int wide_stream(const DevCfg& c, const TmBufs& b, int n, TmSh* sh, uint32_t blk) {
+    const uint32_t mac = (uint32_t)c.max_act_cells;
+    const int per = (n + TM_NT - 1) / TM_NT;
+    const int s0 = (int)threadIdx.x * per;
+    uint32_t cnt = 0;
+    for (int k = 0; k < per && s0 + k < n; k++) cnt += ord_bucket(b.ord_est[s0 + k], mac) >= (uint32_t)b.wide_q ? 1u : 0u;
+    if (threadIdx.x == 0) sh->ti[0] = -1;
+    uint32_t tot;
+    uint32_t r = wg_excl_scan(sh, cnt, &tot);  // (barriers: ti[0] is set before any thread writes it)
+    if (blk < (uint32_t)b.wide_max && blk >= r && blk < r + cnt) {
+        for (int k = 0; k < per && s0 + k < n; k++)
+            if (ord_bucket(b.ord_est[s0 + k], mac) >= (uint32_t)b.wide_q && r++ == blk) sh->ti[0] = s0 + k;
+    }
+    __syncthreads();
+    const int s = sh->ti[0];
+    __syncthreads();
+    return s;
+}
+
+// The step's side of the tail flush: publish stream s's entries logged since
+// its last publication (fx_dupto: published up to) for the next tail launch.
+// Thread 0 only.
+__device__ __forceinline__ void fx_tail_publish(const DevCfg& c, const TmBufs& b, int s, uint32_t dn) {
+    const uint32_t pu = b.fx_dupto[s];
+    if (dn == pu) return;
+    const uint32_t k = atomicAdd(&b.fx_fwork[FX_TCNT + b.fx_tpar], 1u);
+    if (k < (uint32_t)c.n_streams) {
+        b.fx_tjob[(size_t)b.fx_tpar * (uint32_t)c.n_streams + k] = make_uint4((uint32_t)s, pu, dn, 0u);
+        b.fx_dupto[s] = dn;
+    } else {
+        atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);  // (never: one job per stream)
+    }
+}
+
 // Write the inference state back to HBM without reading anything: the
 // infActiveState and infPredictedState bitmaps whole (coalesced 16-byte
 // stores; a step changes the words of ~80 columns of each, which as scattered
@@ -3122,7 +3241,10 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         if (LEARN && (!first || (int)threadIdx.x == sh->ti[1])) hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
     }
     if (threadIdx.x == 0) {
-        if (t.defer) b.fx_dn[s] = t.dn;
+        if (t.defer) {
+            b.fx_dn[s] = t.dn;
+            if (b.fx_tail_wg > 0) fx_tail_publish(c, b, s, t.dn);
+        }
         hdr->avg_input_density = sh->avg_dens;
         hdr->avg_learned_seq_length = sh->avg_lsl;
         hdr->lrn_iter = sh->lrn_iter;
@@ -3214,14 +3336,24 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_AB_KNOBS
     const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    if (FROZEN && direct && b.fx_tail_wg > 0 && blockIdx.x >= (uint32_t)n) {
+        fx_tail_worker(c, b, n, lds);  // (the launch's tail: the deferred-log flush)
+        return;
+    }
     uint32_t u = 0xFFFFFFFFu;
     int s = 0, k = 0, k0 = 0, k1 = 0;
     for (;;) {
         if (k == k1 && direct) {
             if (u != 0xFFFFFFFFu || blockIdx.x >= (uint32_t)n) break;
             u = blockIdx.x;
-            s = b.ord ? (int)__builtin_amdgcn_readfirstlane(b.ord[blockIdx.x]) : (int)blockIdx.x;
-            if (s >= n) break;  // (never: ord is a permutation of the streams)
+            if (b.ord_role == 1) {  // the wide kernel's heavy streams
+                s = wide_stream(c, b, n, reinterpret_cast<TmSh*>(lds), blockIdx.x);
+                if (s < 0) break;
+            } else {
+                if (b.ord_role == 2 && blockIdx.x >= (uint32_t)n - __builtin_amdgcn_readfirstlane(*b.ord_nh)) break;
+                s = b.ord ? (int)__builtin_amdgcn_readfirstlane(b.ord[blockIdx.x]) : (int)blockIdx.x;
+                if (s >= n) break;  // (never: ord lists streams)
+            }
             k0 = k = 0;
             k1 = n_steps;
         }
@@ -3260,12 +3392,14 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_STAMPS
         if (threadIdx.x == 0) reinterpret_cast<TmSh*>(lds)->st_sp0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (!NOSP && !b.tm_only) {
-            if (SPL && sp_learn)
-                sp_step_body<true, PAGED_OK, PAGED_OK || LEARN || HTM_SPL_PLANES>(c, sp, v, s, ssh, keep_overlaps, bkey,
-                                                                                 enc, planes);
-            else sp_step_body<false, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
-            __syncthreads();
+        if constexpr (!NOSP) {  // (TM-only kernels: the SP code is not instantiated)
+            if (!b.tm_only) {
+                if (SPL && sp_learn)
+                    sp_step_body<true, PAGED_OK, PAGED_OK || LEARN || HTM_SPL_PLANES>(c, sp, v, s, ssh, keep_overlaps,
+                                                                                     bkey, enc, planes);
+                else sp_step_body<false, PAGED_OK, true>(c, sp, v, s, ssh, keep_overlaps, nullptr, enc, planes);
+                __syncthreads();
+            }
         }
         tm_step_body<LEARN, FROZEN>(c, b, sp, scores + (size_t)k * c.n_streams, keep_prev, s, lds, k == k0,
                                     k == k1 - 1);
@@ -3328,6 +3462,8 @@ TM_RUN_KERNEL_DECL(run_frozen_paged)
 TM_RUN_KERNEL_DECL(run_learn)
 TM_RUN_KERNEL_DECL(run_learn_tm)
 TM_RUN_KERNEL_DECL(run_infer)
+TM_RUN_KERNEL_DECL(run_wide)
+size_t tmk_wide_lds_bytes(const DevCfg& c);
 // unfused TM step kernels (learn, frozen index, pool scan)
 int tmk_launch_step(int learn, int frozen, int grid, size_t lds, hipStream_t st, DevCfg c, TmBufs b, SpBufs sp,
                     float* scores);
