@@ -515,6 +515,9 @@ def main():
     ap.add_argument("--flush-mode", choices=["auto", "0", "1", "2"], default="auto",
                     help="where the deferred-write flush runs (HTM_OPT_FLUSH_MODE): 0 beside the steps on the "
                          "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
+    ap.add_argument("--flush-every", type=int, default=0,
+                    help="HTM_OPT_FLUSH_EVERY: lockstep steps between the periodic deferred-write flushes (0: the "
+                         "engine default, 8)")
     ap.add_argument("--wide", type=int, default=0,
                     help="HTM_OPT_WIDE: up to N of an ordered launch's heaviest TM steps by 768-thread workgroups "
                          "beside the 256-thread launch (0: off); results identical")
@@ -639,6 +642,8 @@ def main():
         eng.ordered_steps(False)
     if args.wide and not standin:
         eng.wide_steps(args.wide)
+    if args.flush_every and not standin:
+        eng.flush_every(args.flush_every)
     C = args.condition
     # the reference's test phase (SP learning on, TM learning off) on the same
     # engine after the headline and run-mode regions: config 2, Model-1 shape
@@ -775,6 +780,7 @@ def main():
                             if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
                    "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered, "wide": args.wide,
+                   "flush_every": args.flush_every,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
                    "cells_per_column": eng.cells_per_column,
                    "trained_segments": int(hdr.seg_live) if hdr is not None else None,
@@ -866,6 +872,8 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
             child += ["--ordered", args.ordered]
         if args.wide:
             child += ["--wide", str(args.wide)]
+        if args.flush_every:
+            child += ["--flush-every", str(args.flush_every)]
         for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows", "condition"):
             v = getattr(args, k)
             if v is not None:

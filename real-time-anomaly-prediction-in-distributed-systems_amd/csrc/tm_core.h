@@ -115,7 +115,8 @@ enum {
     // (round 5) the learning loops split: update building (active-synapse
     // masks, candidate filters), generator draws (sampling, getCellForNewSegment),
     // segment writes (adapt, trim, create, queued-update appends)
-    SB_LWB, SB_LWS, SB_LWW
+    SB_LWB, SB_LWS, SB_LWW,
+    SB_NCMP  // the normaliser's run-head compaction (frozen ranked tail)
 };
 // event counts: phase2 calls, windows, out-list blocks, qualifying segments, active cells
 // and a histogram of whole-step cycles: SC_HIST + b counts steps of
@@ -1020,18 +1021,33 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
             if (lane_id() == 0) cnt[ch] = (uint32_t)__popcll(m);
         }
         __syncthreads();
+        STAMP(t, SB_NCMP);
         if (wave_id() == 0) {
+            // wave 0 folds the heads from LDS (every lane the same chain, the
+            // reads broadcast): a chain of dependent adds (a readlane per head moved every value through an SGPR,
+            // ~100 cycles each: profiles/r05_mid); entries past a chunk's
+            // count add +0.0f, which leaves the (non-negative) sum unchanged
+            // (16 heads per round: four 16-byte reads issued together, then the
+            // adds -- a chunk holds 64 slots, so reads past its count stay in it)
             float tot = 0.0f;
-            uint32_t n0 = nch ? cnt[0] : 0u;
-            float v0 = nch ? hv[lane_id()] : 0.0f;
+            uint32_t nn1 = nch ? cnt[0] : 0u;
             for (uint32_t ch = 0; ch < nch; ch++) {
-                const uint32_t n1 = ch + 1 < nch ? cnt[ch + 1] : 0u;
-                const float v1 = ch + 1 < nch ? hv[(ch + 1) * 64u + lane_id()] : 0.0f;
-                const int vi = __float_as_int(v0);
-                const uint32_t nn = __builtin_amdgcn_readfirstlane(n0);
-                for (uint32_t j = 0; j < nn; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, (int)j));
-                n0 = n1;
-                v0 = v1;
+                const uint32_t nn = nn1;
+                nn1 = ch + 1 < nch ? cnt[ch + 1] : 0u;
+                const float4* p = reinterpret_cast<const float4*>(hv + ch * 64u);
+                for (uint32_t j = 0; j < nn; j += 16) {
+                    float4 x[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) x[u] = p[(j >> 2) + u];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t k = j + 4u * u;
+                        tot += k < nn ? x[u].x : 0.0f;
+                        tot += k + 1 < nn ? x[u].y : 0.0f;
+                        tot += k + 2 < nn ? x[u].z : 0.0f;
+                        tot += k + 3 < nn ? x[u].w : 0.0f;
+                    }
+                }
             }
             if (lane_id() == 0) sh->tf[0] = tot;
         }
@@ -1237,17 +1253,21 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
     }
     npcol = wg_sum(sh, npcol);
     STAMP(t, SB_SUMS);
-    // total in nonzero-column order (ascending), sequentially as NuPIC sums it:
-    // wave 0 loads 64 column sums at a time and folds them lane by lane
-    // (zero padding adds +0.0f, which leaves the sum unchanged)
+    // total in nonzero-column order (ascending), sequentially as NuPIC sums it
+    // (wave 0, every lane the same chain: eight columns per round, their
+    // indices, then their sums, read before the dependent adds; padding adds
+    // +0.0f)
     if (wave_id() == 0) {
         float tot = 0.0f;
-        for (uint32_t base = 0; base < tnz; base += 64) {
-            const uint32_t i = base + lane_id();
-            const float v = i < tnz ? t.colconf[nzcol[i]] : 0.0f;
-            const int vi = __float_as_int(v);
+        for (uint32_t base = 0; base < tnz; base += 8) {
+            uint32_t ci[8];
+            float v[8];
 #pragma unroll
-            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
+            for (int u = 0; u < 8; u++) ci[u] = base + u < tnz ? nzcol[base + u] : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = base + u < tnz ? t.colconf[ci[u]] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 8; u++) tot += v[u];
         }
         if (lane_id() == 0) sh->tf[0] = tot;
     }
@@ -3313,7 +3333,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
 #define HTM_SPL_PLANES 1
 #endif
 // NOSP compiles the SP out (TM-only launches: the SP kernel ran first)
-template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true, bool NOSP = false>
+template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true, bool NOSP = false, bool WIDE = false>
 __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
                                              float* scores, int n_steps, int sp_learn, int keep_prev,
                                              int keep_overlaps, uint32_t* wq, int unit_steps, int n) {
@@ -3346,7 +3366,7 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
         if (k == k1 && direct) {
             if (u != 0xFFFFFFFFu || blockIdx.x >= (uint32_t)n) break;
             u = blockIdx.x;
-            if (b.ord_role == 1) {  // the wide kernel's heavy streams
+            if constexpr (WIDE) {  // the wide kernel's heavy streams
                 s = wide_stream(c, b, n, reinterpret_cast<TmSh*>(lds), blockIdx.x);
                 if (s < 0) break;
             } else {

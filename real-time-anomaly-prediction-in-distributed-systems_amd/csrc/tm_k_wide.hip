@@ -17,7 +17,7 @@ namespace htm_wide {
 }
 
 __global__ __launch_bounds__(TM_NT) void htm_run_wide_kernel(HTM_RUN_ARGS) {
-    htm_wide::htm_run_body<false, true, false, false, true>(HTM_RUN_PASS);
+    htm_wide::htm_run_body<false, true, false, false, true, true>(HTM_RUN_PASS);
 }
 
 TM_RUN_KERNEL_EXPORTS(run_wide, htm_run_wide_kernel)

@@ -308,7 +308,7 @@ class HTMEngine:
         names = ["load", "phase1", "list", "win_pre", "stream", "qscan", "fin1", "fin2", "backtrack", "learn", "wb",
                  "scan", "sort", "sums", "owner", "sload", "count", "fclr", "pred_cols", "defer", "sp", "norm",
                  "learn_scan", "learn_updates", "learn_wave0", "learn_bt_copy", "compact", "sp_learn",
-                 "lw_build", "lw_draws", "lw_writes"]
+                 "lw_build", "lw_draws", "lw_writes", "norm_compact"]
         cnames = {0: "phase2", 1: "windows", 2: "blocks", 3: "qualifying", 4: "active_cells", 5: "nonzero_cols",
                   6: "steps", 16: "pool_scans", 17: "pool_scan_slots", 18: "sp_row_replays",
                   19: "sp_row_replay_cycles", 20: "sp_row_replay_sample_cycles", 21: "sp_row_replay_skip_cycles",

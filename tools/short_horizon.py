@@ -31,6 +31,8 @@ train = [c for c, m in zip(d["train_cpu"], d["train_mem"]) if not (np.isnan(c) o
 trace = d["test_cpu"].astype(np.float64)
 eng, _, _, _ = bench.trained_engine(rt, N, 72 * 1024, 0, train)
 eng.set_learning(False, False)
+if os.environ.get("SH_FLUSH_EVERY"):
+    eng.flush_every(int(os.environ["SH_FLUSH_EVERY"]))
 if os.environ.get("SH_WIDE"):
     eng.wide_steps(int(os.environ["SH_WIDE"]))
 if os.environ.get("SH_FLUSH_MODE"):
@@ -59,7 +61,7 @@ for r in range(REGIONS):
     flush.append(ev[STEPS].elapsed_time(ev[STEPS + 1]))
     k0 += STEPS
 ps = np.median(np.array(per_step), axis=0)
-out = {"flush_mode": os.environ.get("SH_FLUSH_MODE", "default"), "steps": STEPS, "warmup": WARM, "condition": COND, "regions": REGIONS,
+out = {"flush_mode": os.environ.get("SH_FLUSH_MODE", "default"), "flush_every": os.environ.get("SH_FLUSH_EVERY", "default"), "steps": STEPS, "warmup": WARM, "condition": COND, "regions": REGIONS,
        "wall_ms_per_step_median": round(float(np.median(wall)) / STEPS, 4),
        "wall_ms_per_step_each_region": [round(w / STEPS, 4) for w in wall],
        "step_ms_median_by_position": [round(float(x), 4) for x in ps],
