@@ -2,6 +2,8 @@
 // kernels, the frozen-index build (rank / count / fill) and the deferred
 // dutyCycle() flush.  The step kernels themselves are in tm_k_*.hip, their
 // device code in tm_core.h (BacktrackingTM + raw anomaly, see its header).
+#include <algorithm>
+
 #include "tm_core.h"
 
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).total; }
@@ -331,7 +333,11 @@ int tm_configure_lds(const DevCfg& c) {
     int r = tmk_attr_step(b0, b1, b2);
     r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1) |
          tmk_attr_run_frozen_spl(b1) | tmk_attr_run_learn_tm(b0);
+#ifdef HTM_WIDE_LDS_MIN
+    r |= tmk_attr_run_wide(std::max(tmk_wide_lds_bytes(c), (size_t)HTM_WIDE_LDS_MIN));
+#else
     r |= tmk_attr_run_wide(tmk_wide_lds_bytes(c));
+#endif
     r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
                  hipSuccess ? 0 : -1;
     (void)hipGetLastError();

@@ -373,6 +373,37 @@ __device__ __forceinline__ bool infer_phase1(Tm& t, const uint16_t* cols, int nA
 #ifndef SC_DEPTH
 #define SC_DEPTH 8
 #endif
+// one segment's lane of a pool scan: the mask of its synapses (this lane's
+// eight) onto cells on in `state`, OR-ed over the segment's four lanes
+__device__ __forceinline__ uint32_t scan_seg_mask(const uint32_t* state, uint32_t cwm1, uint32_t sub, uint32_t m,
+                                                  bool el, uint4 v, uint32_t& nb) {
+    const uint32_t nsyn = meta_nsyn(m);
+    uint32_t mask = 0;
+    if (el && sub * 8u < nsyn) {
+        nb += 16;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        // all eight state words read unconditionally (one LDS round trip; a
+        // per-synapse `j < nsyn &&` test made a branch and a wait per read),
+        // entries past nsyn clamped into the bitmap and masked off afterwards
+        uint32_t sw[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t wi = (w[k >> 1] >> ((k & 1) * 16 + 5)) & 0x7FFu;
+            sw[k] = state[wi < cwm1 ? wi : cwm1];
+        }
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) bits |= ((sw[k] >> ((w[k >> 1] >> ((k & 1) * 16)) & 31u)) & 1u) << k;
+        const uint32_t left = nsyn - sub * 8u;
+        mask = (bits & (left >= 8u ? 0xFFu : (1u << left) - 1u)) << (sub * 8u);
+    }
+    // OR over the segment's four lanes: DPP quad permutes (a __shfl_xor is a
+    // ds_bpermute, an LDS round trip)
+    mask |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mask, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    mask |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mask, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    return mask;
+}
+
 template <bool SPEC = false, typename E, typename F>
 __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E elig, F f) {
     const uint32_t hwm = t.sh->hwm;
@@ -411,31 +442,7 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
         for (int d = 0; d < SC_DEPTH; d++) {
             const uint32_t slot = base + d * (TM_NT / 4) + g;
             if (slot < hwm && sub == 0) nb += 4;
-            const uint32_t nsyn = meta_nsyn(m[d]);
-            uint32_t mask = 0;
-            if (el[d] && sub * 8u < nsyn) {
-                nb += 16;
-                const uint32_t w[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
-                // all eight state words read unconditionally (one LDS round
-                // trip; a per-synapse `j < nsyn &&` test made a branch and a
-                // wait per read), entries past nsyn clamped into the bitmap and
-                // masked off afterwards
-                uint32_t sw[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t wi = (w[k >> 1] >> ((k & 1) * 16 + 5)) & 0x7FFu;
-                    sw[k] = state[wi < cwm1 ? wi : cwm1];
-                }
-                uint32_t bits = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) bits |= ((sw[k] >> ((w[k >> 1] >> ((k & 1) * 16)) & 31u)) & 1u) << k;
-                const uint32_t left = nsyn - sub * 8u;
-                mask = (bits & (left >= 8u ? 0xFFu : (1u << left) - 1u)) << (sub * 8u);
-            }
-            // OR over the segment's four lanes: DPP quad permutes (a __shfl_xor
-            // is a ds_bpermute, an LDS round trip)
-            mask |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mask, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-            mask |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mask, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+            const uint32_t mask = scan_seg_mask(state, cwm1, sub, m[d], el[d], v[d], nb);
             f(slot, m[d], el[d], mask);
         }
     }
@@ -536,19 +543,6 @@ __device__ __forceinline__ void fx_qualify(const uint32_t* cnt, uint32_t nbytes,
 // sweeps a contiguous run of quads; one workgroup scan places the runs), so
 // the qualifying list comes out in rank = (cell, creation) order.  Counters
 // never exceed 32 (see fx_qualify).  Contains barriers: call uniformly.
-// 16-bit hit mask of one counter quad: bit 4j+i set when byte i of word j
-// is >= thr (add = 0x01010101 * (128 - thr); counters never exceed 32)
-__device__ __forceinline__ uint32_t fx_quad_hits(uint4 x, uint32_t add) {
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-    uint32_t h = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t m = (w[j] + add) & 0x80808080u;
-        h |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
-    }
-    return h;
-}
-
 #ifndef FX_CQ
 #define FX_CQ 16  // counter quads one thread sweeps (W <= 16 x 16 x TM_NT bytes)
 #endif
@@ -559,17 +553,24 @@ __device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t
     const uint4* c4 = reinterpret_cast<const uint4*>(cnt);
     const uint32_t per = (nquads + TM_NT - 1) / TM_NT;  // <= FX_CQ (fx_win <= 64512)
     const uint32_t q0 = threadIdx.x * per;
-    // one sweep: every quad of the thread's run loaded at once, its hits kept
-    // as 16-bit masks (two per register)
-    uint32_t hm[FX_CQ / 2];
-    uint32_t mine = 0;
+    // one sweep: every quad of the thread's run loaded at once; the hits of a
+    // quad counted from its masked words (byte + (128 - thr) sets bit 7
+    // exactly when byte >= thr), and only a bit per quad kept -- hits are
+    // rare (a few hundred of the window's ranks), so the quads that have
+    // them are read again to place them
+    uint32_t any = 0, mine = 0;
+    const uint32_t nq = q0 < nquads ? (nquads - q0 < per ? nquads - q0 : per) : 0u;
+    for (uint32_t i0 = 0; i0 < nq; i0 += 4) {  // (four quads' reads in flight)
+        uint4 x[4];
 #pragma unroll
-    for (int i = 0; i < FX_CQ; i++) {
-        uint32_t h = 0;
-        if ((uint32_t)i < per && q0 + i < nquads) h = fx_quad_hits(c4[q0 + i], add);
-        if (i & 1) hm[i >> 1] |= h << 16;
-        else hm[i >> 1] = h;
-        mine += __popc(h);
+        for (int u = 0; u < 4; u++) x[u] = i0 + u < nq ? c4[q0 + i0 + u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t h = __popc((x[u].x + add) & 0x80808080u) + __popc((x[u].y + add) & 0x80808080u) +
+                               __popc((x[u].z + add) & 0x80808080u) + __popc((x[u].w + add) & 0x80808080u);
+            mine += h;
+            any |= (h ? 1u : 0u) << (i0 + u);
+        }
     }
     // exclusive prefix over the workgroup in thread order (one barrier)
     const uint32_t qn0 = (uint32_t)sh->qn;  // thread 0 updates it only after the barrier
@@ -583,12 +584,15 @@ __device__ __forceinline__ void fx_collect_ordered(const uint32_t* cnt, uint32_t
         if (v < (int)wave_id()) pos += x;
         tot += x;
     }
-    if (mine) {
+    for (uint32_t a = any; a; a &= a - 1) {
+        const uint32_t i = __ffs(a) - 1;
+        const uint4 x = c4[q0 + i];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-        for (int i = 0; i < FX_CQ; i++) {
-            for (uint32_t m = (hm[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; m; m &= m - 1) {
-                const uint32_t b = __ffs(m) - 1;  // 4 * word + byte
-                if (pos < qcap) dst[pos] = base + 16 * (q0 + i) + b;
+        for (int j = 0; j < 4; j++) {
+            for (uint32_t m = (w[j] + add) & 0x80808080u; m; m &= m - 1) {
+                const uint32_t b = (uint32_t)(__ffs(m) - 1) >> 3;  // byte of the word
+                if (pos < qcap) dst[pos] = base + 16 * (q0 + i) + 4 * j + b;
                 pos++;
             }
         }
@@ -1253,21 +1257,19 @@ __device__ __forceinline__ uint32_t phase2_finish(Tm& t) {
     }
     npcol = wg_sum(sh, npcol);
     STAMP(t, SB_SUMS);
-    // total in nonzero-column order (ascending), sequentially as NuPIC sums it
-    // (wave 0, every lane the same chain: eight columns per round, their
-    // indices, then their sums, read before the dependent adds; padding adds
-    // +0.0f)
+    // total in nonzero-column order (ascending), sequentially as NuPIC sums it:
+    // wave 0 loads 64 column sums at a time and folds them lane by lane
+    // (zero padding adds +0.0f, which leaves the sum unchanged; a one-lane
+    // fold reading them from LDS measured slower here: fin2 8 K -> 28 K cycles
+    // per learning stream-step, profiles/r05_ab)
     if (wave_id() == 0) {
         float tot = 0.0f;
-        for (uint32_t base = 0; base < tnz; base += 8) {
-            uint32_t ci[8];
-            float v[8];
+        for (uint32_t base = 0; base < tnz; base += 64) {
+            const uint32_t i = base + lane_id();
+            const float v = i < tnz ? t.colconf[nzcol[i]] : 0.0f;
+            const int vi = __float_as_int(v);
 #pragma unroll
-            for (int u = 0; u < 8; u++) ci[u] = base + u < tnz ? nzcol[base + u] : 0u;
-#pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = base + u < tnz ? t.colconf[ci[u]] : 0.0f;
-#pragma unroll
-            for (int u = 0; u < 8; u++) tot += v[u];
+            for (int j = 0; j < 64; j++) tot += __int_as_float(__builtin_amdgcn_readlane(vi, j));
         }
         if (lane_id() == 0) sh->tf[0] = tot;
     }

@@ -27,6 +27,11 @@ size_t tmk_wide_lds_bytes(const DevCfg& c) { return htm_wide::tm_layout(c, 0, 1)
 int launch_htm_run_wide(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
                         int n, int grid, hipStream_t st) {
     if (n <= 0 || grid <= 0 || b.ord_role != 1 || !b.ord_est || b.wide_q < 0 || b.wide_q >= ORD_NB) return -1;
-    return tmk_launch_run_wide(grid, tmk_wide_lds_bytes(c), st, c, b, sp, values, scores, 1, 0, 0, 0, nullptr, 1,
-                               n);
+    size_t lds = tmk_wide_lds_bytes(c);
+#ifdef HTM_WIDE_LDS_MIN
+    // (experiment builds: a 256-thread heavy-step kernel kept alone on its CU
+    // by its LDS request)
+    if (lds < (size_t)HTM_WIDE_LDS_MIN) lds = (size_t)HTM_WIDE_LDS_MIN;
+#endif
+    return tmk_launch_run_wide(grid, lds, st, c, b, sp, values, scores, 1, 0, 0, 0, nullptr, 1, n);
 }
