@@ -901,6 +901,10 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
     kernels = pmc_summary.summarise(os.path.join(out, "run"))
     path = os.path.join(out, "pmc_summary.json")
     json.dump({"source": out, "kernels": kernels}, open(path, "w"), indent=1)
+    keep = os.environ.get("HTM_BENCH_PMC_KEEP")  # a directory to keep a copy of the summary in
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+        shutil.copy(path, os.path.join(keep, "pmc_summary_%s.json" % ("learn_on" if learn_leg else "config%d" % args.config)))
     return path, None
 
 
