@@ -479,10 +479,12 @@ def main():
     ap.add_argument("--seg-capacity", type=int, default=None, help="segment slots per stream")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
-    ap.add_argument("--profile-every", type=int, default=4,
+    ap.add_argument("--profile-every", type=int, default=5,
                     help="HIP events around every N-th launch of the timed region (HTM_OPT_PROFILE N; a timed "
                          "event record between dependent launches holds the queue ~12 us, so the roofline's "
-                         "launch time is averaged over a sample: default every 4th)")
+                         "launch time is averaged over a sample: default every 5th -- prime to the deferred "
+                         "flush's 8-step cadence, whose following launch runs beside the flush: every 4th "
+                         "sampled that launch in half its samples, profiles/r05_ab/README.md)")
     ap.add_argument("--mode", choices=["step", "run"], default="step",
                     help="step (default, the headline): lockstep -- one htm_step per step, every stream "
                          "advances one network.run(1) per step (north_star's real-time stepping); run: the K "
