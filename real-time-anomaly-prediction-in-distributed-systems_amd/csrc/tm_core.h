@@ -478,24 +478,34 @@ __device__ __forceinline__ void fx_count_block(uint32_t* cnt, uint4 v, uint32_t 
     }
 }
 
+// block -> list map of the blocks [lo, hi): owner[x - lo] = the list holding block x
+__device__ __forceinline__ void fx_owner_map(const uint32_t* pstart, uint32_t na, uint32_t lo, uint32_t hi,
+                                             uint16_t* owner) {
+    for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
+        const uint32_t a = pstart[k] > lo ? pstart[k] : lo;
+        const uint32_t z = pstart[k + 1] < hi ? pstart[k + 1] : hi;
+        for (uint32_t x = a; x < z; x++) owner[x - lo] = (uint16_t)k;
+    }
+}
+
 // Stream the 16-byte blocks of lists k < na -- list k is the block range
 // [plo[k], plo[k] + n_k) of ent, pstart the exclusive prefix of n_k with
 // pstart[na] = B -- and count every u16 entry into the u8 counters.  Per
-// pass a block -> list map is built in LDS, then every thread issues its
-// FX_DEPTH block loads before counting any, so one HBM round trip covers
-// FX_OWN blocks whatever the list lengths.
+// pass of FX_OWN blocks every thread issues its FX_DEPTH block loads (their
+// lists from a block -> list map in LDS) before counting any, so one HBM
+// round trip covers FX_OWN blocks whatever the list lengths; the next pass's
+// map is built while those loads are in flight (a barrier once every thread
+// has read the map for its addresses -- LDS reads only: the loads stay in
+// flight), not before the next loads.
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
                                           uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy,
                                           TmSh* shp = nullptr) {
+    if (B == 0) return;
+    fx_owner_map(pstart, na, 0u, B < FX_OWN ? B : FX_OWN, owner);
+    __syncthreads();
+    STAMP_SH(shp, SB_OWNER);
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
-        for (uint32_t k = threadIdx.x; k < na; k += TM_NT) {
-            const uint32_t a = pstart[k] > lo ? pstart[k] : lo;
-            const uint32_t z = pstart[k + 1] < hi ? pstart[k + 1] : hi;
-            for (uint32_t x = a; x < z; x++) owner[x - lo] = (uint16_t)k;
-        }
-        __syncthreads();
-        STAMP_SH(shp, SB_OWNER);
         uint4 v[FX_DEPTH];
 #pragma unroll
         for (int j = 0; j < FX_DEPTH; j++) {
@@ -506,6 +516,9 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
                 v[j] = ent[plo[k] + (x - pstart[k])];
             }
         }
+        __syncthreads();  // (every thread's map reads done)
+        if (hi < B) fx_owner_map(pstart, na, hi, B - hi < FX_OWN ? B : hi + FX_OWN, owner);
+        STAMP_SH(shp, SB_OWNER);
 #pragma unroll
         for (int j = 0; j < FX_DEPTH; j++) {
 #ifdef HTM_STAMPS
