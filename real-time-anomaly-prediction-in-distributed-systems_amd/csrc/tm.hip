@@ -454,96 +454,42 @@ int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, 
 }
 
 // Before a flush (on the flush's stream): the entries [fx_dflushed, fx_dsnap)
-// of every stream as a compact job list, without repeats -- an entry whose
-// active set equals an earlier entry of the same batch (order-independent
-// hash and length first, then the cells themselves) is dropped: the flush of
-// the earlier one makes the same one-time record writes.  Steps append to the
-// ring beside this kernel but never into [fx_dflushed, fx_dsnap), so the
-// batch is stable.  The bound taken is stored in fx_dupto: a later snapshot
-// the step stream takes while this flush runs (flushes every few steps, a
-// flush slower than that) moves fx_dsnap, not what this flush completes --
-// its done kernel advances fx_dflushed to fx_dupto, so no entry is marked
-// flushed without having been replayed.  One workgroup per stream.
+// of every stream as a compact job list.  Steps append to the ring beside
+// this kernel but never into [fx_dflushed, fx_dsnap), so the batch is stable.
+// The bound taken is stored in fx_dupto: a later snapshot the step stream
+// takes while this flush runs (flushes every few steps, a flush slower than
+// that) moves fx_dsnap, not what this flush completes -- its done kernel
+// advances fx_dflushed to fx_dupto, so no entry is marked flushed without
+// having been replayed.  One thread per stream.  No repeats to drop: a step
+// logs no set equal to one still in the ring (defer_phase2), and the ring
+// holds more entries than a batch (round 4 hashed every batch's cells here to
+// find repeats; it found none -- 14.7 us of every flush's critical path).
 // from_dn: the flush runs on the step stream after the steps (nothing appends
 // meanwhile), so the bound is fx_dn itself -- no snapshot launch.
 __global__ __launch_bounds__(256) void tm_fx_jobs_kernel(DevCfg c, TmBufs b, int n, int from_dn, int split) {
-    __shared__ uint32_t hsh[64], len[64], keep[64];
-    const int s = blockIdx.x;
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
     const uint32_t dcap = (uint32_t)c.fx_dcap;
     const uint32_t f = b.fx_dflushed[s], u = from_dn ? b.fx_dn[s] : b.fx_dsnap[s], p = u - f;
     // the ring invariant: fx_dflushed <= fx_dsnap <= fx_dflushed + fx_dcap
     // (a step appends only while fewer than fx_dcap entries are unflushed)
-    const bool bad = p > dcap || dcap > 64u;
-    if (threadIdx.x == 0) {
-        b.fx_dupto[s] = bad ? f : u;
-        if (bad) atomicOr(&b.fx_fwork[1], FX_ERR_RING);
-    }
+    const bool bad = p > dcap;
+    b.fx_dupto[s] = bad ? f : u;
+    if (bad) atomicOr(&b.fx_fwork[1], FX_ERR_RING);
     if (p == 0 || bad) return;
-    const size_t mac = fx_dstride(c);
-    auto entry = [&](uint32_t i) { return (size_t)s * dcap + (f + i) % dcap; };
-    if (threadIdx.x < p) {
-        hsh[threadIdx.x] = 0u;
-        const uint32_t l = b.fx_dlen[entry(threadIdx.x)];
-        len[threadIdx.x] = l < (uint32_t)mac ? l : (uint32_t)mac;  // (a longer one is flagged by the flush)
-    }
-    __syncthreads();
+    // one job per entry, or per (entry, rank window of the stream's model) when split
+    const uint32_t nwin = (uint32_t)c.fx_nwin, W = (uint32_t)c.fx_win;
+    const uint32_t nr = b.fx_nr[model_stream(c, s)];
+    uint32_t nw = (nr + W - 1u) / W;
+    nw = nw < nwin ? nw : nwin;
+    if (!split) nw = 1u;
+    uint32_t base = atomicAdd(&b.fx_fwork[2], p * nw);
+    const uint32_t cap = (uint32_t)n * dcap * nwin;
     for (uint32_t i = 0; i < p; i++) {
-        const uint16_t* cl = b.fx_dlog + entry(i) * mac;
-        uint32_t h = 0;
-        for (uint32_t k = threadIdx.x; k < len[i]; k += blockDim.x) h += fmix32(cl[k] + 0x9e3779b9u);
-        h = wave_sum_u32(h);
-        if (lane_id() == 0 && h) atomicAdd(&hsh[i], h);
-    }
-    __syncthreads();
-    if (threadIdx.x < p) {
-        const uint32_t i = threadIdx.x, li = len[i];
-        const uint16_t* ci = b.fx_dlog + entry(i) * mac;
-        uint32_t dup = 0;
-        for (uint32_t j = 0; j < i && !dup; j++) {
-            if (hsh[j] != hsh[i] || len[j] != li) continue;
-            const uint16_t* cj = b.fx_dlog + entry(j) * mac;
-            // 8 cells per 16-byte load, four loads in flight (slots are 16-byte
-            // aligned: max_act_cells is a multiple of 8)
-            const uint4* qi = reinterpret_cast<const uint4*>(ci);
-            const uint4* qj = reinterpret_cast<const uint4*>(cj);
-            const uint32_t nq = li / 8;
-            uint32_t diff = 0;
-            for (uint32_t q = 0; q < nq && !diff; q += 4) {
-                uint4 a[4], z[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    a[u] = q + u < nq ? qi[q + u] : make_uint4(0u, 0u, 0u, 0u);
-                    z[u] = q + u < nq ? qj[q + u] : make_uint4(0u, 0u, 0u, 0u);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    diff |= (a[u].x ^ z[u].x) | (a[u].y ^ z[u].y) | (a[u].z ^ z[u].z) | (a[u].w ^ z[u].w);
-            }
-            for (uint32_t k = nq * 8; k < li && !diff; k++) diff = ci[k] != cj[k];
-            dup = diff ? 0u : 1u;
-        }
-        keep[i] = dup ? 0u : 1u;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        // one job per kept entry, or per (kept entry, rank window of the
-        // stream's model) when split
-        const uint32_t nwin = (uint32_t)c.fx_nwin, W = (uint32_t)c.fx_win;
-        const uint32_t nr = b.fx_nr[model_stream(c, s)];
-        uint32_t nw = (nr + W - 1u) / W;
-        nw = nw < nwin ? nw : nwin;
-        if (!split) nw = 1u;
-        uint32_t m = 0;
-        for (uint32_t i = 0; i < p; i++) m += keep[i];
-        uint32_t base = atomicAdd(&b.fx_fwork[2], m * nw);
-        const uint32_t cap = (uint32_t)n * dcap * nwin;
-        for (uint32_t i = 0; i < p; i++) {
-            if (!keep[i]) continue;
-            const uint32_t e = (uint32_t)s * dcap + (f + i) % dcap;
-            for (uint32_t w = 0; w < nw; w++, base++) {
-                if (base < cap) b.fx_fjobs[base] = e * (nwin + 1u) + (split ? w : nwin);
-                else atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
-            }
+        const uint32_t e = (uint32_t)s * dcap + (f + i) % dcap;
+        for (uint32_t w = 0; w < nw; w++, base++) {
+            if (base < cap) b.fx_fjobs[base] = e * (nwin + 1u) + (split ? w : nwin);
+            else atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);
         }
     }
 }
@@ -580,7 +526,7 @@ int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipS
     int grid = run_grid((const void*)tm_fx_flush_kernel, lds, total);
     if (grid > FX_FLUSH_WG) grid = FX_FLUSH_WG;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
-    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3(n), dim3(256), 0, st, c, b, n, from_dn, split);
+    hipLaunchKernelGGL(tm_fx_jobs_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c, b, n, from_dn, split);
     hipLaunchKernelGGL(tm_fx_flush_kernel, dim3(grid), dim3(TM_NT), lds, st, c, b, n);
     hipLaunchKernelGGL(tm_fx_flush_done_kernel, dim3((n + 255) / 256), dim3(256), 0, st, b, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
