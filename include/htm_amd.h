@@ -177,7 +177,8 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    save, learning on, htm_status / htm_counters, htm_flush.  Results and
                                    state are those of the undeferred step.  0: count every phase 2 in full */
 #define HTM_OPT_FLUSH_MODE 11   /* where the deferred-write flush runs: 0 on the engine's own HIP stream
-                                   beside the next steps, 1 on the step stream after them (full width).
+                                   beside the next steps, 1 on the step stream after them (full width),
+                                   2 in the tail workgroups of the next ordered launch (other launches as 0).
                                    Results are identical; the default is chosen by measurement from the
                                    engine size (deferred dutyCycle() writes) */
 #define HTM_OPT_ORDERED 12      /* 1 (default): a frozen lockstep step (htm_step) of a dense-SP engine of
