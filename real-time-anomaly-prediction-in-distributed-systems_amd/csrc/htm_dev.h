@@ -102,7 +102,9 @@ __host__ __device__ inline size_t fx_dstride(const DevCfg& c) { return ((size_t)
 
 #define RDSE_HDR_WORDS 64   // int32 words of an RDSE field header (HTM_ST_ENC_RDSE)
 
-#define SP_CKPT_COLS 8      // columns per SP-initialisation checkpoint (paged permanences)
+#ifndef SP_CKPT_COLS
+#define SP_CKPT_COLS 8      // columns per SP-initialisation checkpoint (paged permanences; <= 8)
+#endif
 #define SP_CKPT_WORDS 64    // words per checkpoint: st[31], idx, pending draws buf[31], pad
 #define SP_ROW_NONE 0xFFFFFFFFu
 #define SP_ERR_POOL 32u     // error flag: paged SP row pool exhausted (results invalid)

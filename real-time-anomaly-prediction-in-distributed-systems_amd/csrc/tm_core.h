@@ -449,6 +449,75 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
     return nb;
 }
 
+// A scan whose eligible segments are few (learn phase 1: the segments of a
+// handful of flagged columns): the meta words are streamed SCS_META per thread
+// per round trip and the eligible slots listed in LDS (elist[0] the count,
+// elist[1..ecap] the slots), then only their rows are read, four lanes per
+// segment -- two or three round trips for the pool instead of two per
+// SC_DEPTH x 64 slots.  f(slot, meta, true, mask) for the eligible slots only
+// (the callers ignore ineligible ones).  Sets *overflow (uniform) and calls no
+// f when more than ecap slots are eligible: the caller then runs scan_pool.
+// Contains barriers: call uniformly.  Returns this thread's bytes.
+#ifndef SCS_META
+#define SCS_META 16
+#endif
+template <typename E, typename F>
+__device__ __forceinline__ uint32_t scan_pool_sparse(Tm& t, const uint32_t* state, E elig, F f, uint32_t* elist,
+                                                     uint32_t ecap, bool* overflow) {
+    const uint32_t hwm = t.sh->hwm;
+    COUNT(t, SC_NSCAN, 1);
+    COUNT(t, SC_SCANSLOTS, hwm);
+    uint32_t nb = 0;
+    if (threadIdx.x == 0) elist[0] = 0u;
+    __syncthreads();
+    for (uint32_t base = 0; base < hwm; base += SCS_META * TM_NT) {
+        uint32_t m[SCS_META];
+#pragma unroll
+        for (int d = 0; d < SCS_META; d++) {
+            const uint32_t slot = base + d * TM_NT + threadIdx.x;
+            m[d] = slot < hwm ? t.meta[slot] : 0u;
+        }
+#pragma unroll
+        for (int d = 0; d < SCS_META; d++) {
+            const uint32_t slot = base + d * TM_NT + threadIdx.x;
+            if (slot < hwm) nb += 4;
+            if (meta_live(m[d]) && elig(m[d])) {
+                const uint32_t k = atomicAdd(&elist[0], 1u);
+                if (k < ecap) elist[1 + k] = slot;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t ne = elist[0];
+    *overflow = ne > ecap;
+    if (ne > ecap) return nb;
+    const uint32_t g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    const uint32_t cwm1 = (uint32_t)t.c.cw - 1u;
+    for (uint32_t e0 = 0; e0 < ne; e0 += 2u * (TM_NT / 4)) {  // (two segments per quad in flight)
+        uint32_t sl[2], mm[2];
+        uint4 v[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t e = e0 + (uint32_t)u * (TM_NT / 4) + g;
+            sl[u] = e < ne ? elist[1 + e] : 0u;
+            mm[u] = e < ne ? t.meta[sl[u]] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            v[u] = sub * 8u < meta_nsyn(mm[u])
+                       ? *reinterpret_cast<const uint4*>(t.src + (size_t)sl[u] * HTM_MAXSYN + sub * 8)
+                       : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t e = e0 + (uint32_t)u * (TM_NT / 4) + g;
+            const bool in = e < ne;
+            const uint32_t mask = scan_seg_mask(state, cwm1, sub, mm[u], in, v[u], nb);
+            if (in) f(sl[u], mm[u], true, mask);
+        }
+    }
+    return nb;
+}
+
 // collect slots of segments with >= thr synapses onto active cells of
 // `state` by scanning the pool (learning-on form)
 __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
@@ -1573,14 +1642,21 @@ __device__ __forceinline__ void scan_best(Tm& t, const uint32_t* state, int thr,
         }
     };
     // every column (learn phase 2): rows loaded with the meta words; flagged
-    // columns only (learn phase 1): rows of those columns' segments only
-    uint32_t nb = colflags ? scan_pool<false>(t, state,
-                                              [&](uint32_t m) {
-                                                  const uint32_t col = col_of(c, meta_cell(m));
-                                                  return ((colflags[col >> 5] >> (col & 31)) & 1u) != 0u;
-                                              },
-                                              best)
-                           : scan_pool<true>(t, state, [](uint32_t) { return true; }, best);
+    // columns only (learn phase 1): the eligible slots listed first (in the
+    // learning records' LDS, free until the records are built), then their
+    // rows -- the whole pool's scan only if the list overflows
+    auto flagged = [&](uint32_t m) {
+        const uint32_t col = col_of(c, meta_cell(m));
+        return ((colflags[col >> 5] >> (col & 31)) & 1u) != 0u;
+    };
+    uint32_t nb;
+    if (colflags) {
+        bool over = false;
+        nb = scan_pool_sparse(t, state, flagged, best, t.U + 2 * c.ncol, (uint32_t)LREC_WORDS - 1u, &over);
+        if (over) nb += scan_pool<false>(t, state, flagged, best);
+    } else {
+        nb = scan_pool<true>(t, state, [](uint32_t) { return true; }, best);
+    }
     nb = wg_sum(t.sh, nb);
     if (threadIdx.x == 0) t.sh->bytes += nb;
 }
