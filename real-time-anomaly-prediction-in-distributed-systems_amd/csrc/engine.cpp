@@ -392,6 +392,30 @@ static int dalloc(htm_engine* e, void** p, size_t bytes) {
         field = reinterpret_cast<T*>(p_);                                          \
     } while (0)
 
+// B^(2^p), p < SP_JUMP_POW, of the block map st[(3 + j) % 31] += st[j] (j = 0..30),
+// row j column i = the weight of st[i] in the new st[j]; rows padded to 32 words
+static void sp_jump_tables(std::vector<uint32_t>& out) {
+    std::vector<uint32_t> m(31 * 31), t(31 * 31);
+    for (int i = 0; i < 31; i++) {
+        uint32_t st[31] = {0};
+        st[i] = 1u;
+        for (int j = 0; j < 31; j++) st[(3 + j) % 31] += st[j];
+        for (int j = 0; j < 31; j++) m[j * 31 + i] = st[j];
+    }
+    out.assign((size_t)SP_JUMP_POW * 31 * 32, 0u);
+    for (int p = 0; p < SP_JUMP_POW; p++) {
+        for (int j = 0; j < 31; j++)
+            for (int i = 0; i < 31; i++) out[((size_t)p * 31 + j) * 32 + i] = m[j * 31 + i];
+        for (int j = 0; j < 31; j++)  // m = m * m (mod 2^32)
+            for (int i = 0; i < 31; i++) {
+                uint32_t a = 0;
+                for (int k = 0; k < 31; k++) a += m[j * 31 + k] * m[k * 31 + i];
+                t[j * 31 + i] = a;
+            }
+        m.swap(t);
+    }
+}
+
 static int allocate(htm_engine* e) {
     const DevCfg& d = e->dc;
     const size_t S = (size_t)e->n;
@@ -407,6 +431,16 @@ static int allocate(htm_engine* e) {
         ALLOC(e->sp.pool, float, (size_t)d.pool_rows * d.pool_stride);
         ALLOC(e->sp.pool_next, unsigned long long, 1);
         ALLOC(e->sp.ckpt, uint32_t, M * d.n_ckpt * SP_CKPT_WORDS);
+        {
+            // jump tables of the replays' skip (sp_jump_blocks): B^(2^p), B the
+            // 31-draw block map of nupic::Random's state, linear over Z/2^32
+            std::vector<uint32_t> jt;
+            sp_jump_tables(jt);
+            uint32_t* dj = nullptr;
+            ALLOC(dj, uint32_t, jt.size());
+            HIP_TRY(hipMemcpy(dj, jt.data(), jt.size() * 4, hipMemcpyHostToDevice));
+            e->sp.jump = dj;
+        }
     } else {
         ALLOC(e->sp.perm, float, M * d.ncol * d.n_potential);
     }

@@ -102,6 +102,7 @@ __host__ __device__ inline size_t fx_dstride(const DevCfg& c) { return ((size_t)
 
 #define RDSE_HDR_WORDS 64   // int32 words of an RDSE field header (HTM_ST_ENC_RDSE)
 
+#define SP_JUMP_POW 16      // jump tables: skips of up to 2^16 - 1 blocks (an 8-column group needs < 2^10)
 #ifndef SP_CKPT_COLS
 #define SP_CKPT_COLS 8      // columns per SP-initialisation checkpoint (paged permanences; <= 8)
 #endif
@@ -129,6 +130,8 @@ struct SpBufs {
     float* pool;        // [pool_rows][pool_stride]
     unsigned long long* pool_next;  // [1] rows handed out
     uint32_t* ckpt;     // [S][n_ckpt][SP_CKPT_WORDS] RNG state at columns 0, 8, 16, ... of sp_init
+    const uint32_t* jump;  // [SP_JUMP_POW][31][32] the 31-draw block map of nupic::Random raised to 2^p
+                           //     (rows padded to 32 words): skipping whole blocks by matrix powers
     uint32_t* err;      // [S] SP error flags (SP_ERR_POOL)
     float* boost;       // [S][ncol] boostFactors_ (1.0 at init)
     // RDSE encoders (DevCfg::enc_type == HTM_ENC_RDSE): per stream, per field

@@ -349,10 +349,43 @@ struct SpInitCfg {
     float sp_conn, sp_trim, sp_conn_thr;
     const uint32_t* potmask;
     const uint32_t* ckpt;
+    const uint32_t* jump;  // SpBufs::jump (null: skip block by block)
 };
 __device__ __forceinline__ SpInitCfg sp_init_cfg(const DevCfg& c, const SpBufs& b) {
     return SpInitCfg{c.nin, c.nin_pad, c.ncol, c.n_potential, c.n_ckpt, c.sp_conn, c.sp_trim, c.sp_conn_thr,
-                     b.potmask, b.ckpt};
+                     b.potmask, b.ckpt, b.jump};
+}
+
+// Advance the generator (st: the 31-word state in sp_regen_row's form,
+// wave-uniform) by nbk whole blocks of 31 draws at once.  The block map
+// (st[(3 + j) % 31] += st[j], j = 0..30) is linear over Z/2^32, so nbk blocks
+// are the product of the tabled powers B^(2^p) of nbk's set bits: lane j
+// computes the new word j as row j of the matrix times the state (31
+// multiply-adds, the state read from the lanes) -- a few matrix-vector
+// products instead of nbk x 31 dependent scalar adds (the paged replays'
+// skip was 63 % of their cycles, profiles/r05_learn).  Call with every lane.
+__device__ __forceinline__ void sp_jump_blocks(uint32_t (&st)[31], uint32_t nbk, const uint32_t* jump) {
+    const uint32_t l = (uint32_t)lane_id();
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 31; j++) x = l == (uint32_t)j ? st[j] : x;
+    for (uint32_t p = 0; nbk != 0u && p < SP_JUMP_POW; p++, nbk >>= 1) {
+        if (!(nbk & 1u)) continue;
+        const uint4* row = reinterpret_cast<const uint4*>(jump + ((size_t)p * 31u + (l < 31u ? l : 30u)) * 32u);
+        uint4 r[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) r[q] = row[q];
+        const uint32_t w[32] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
+                                r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w,
+                                r[4].x, r[4].y, r[4].z, r[4].w, r[5].x, r[5].y, r[5].z, r[5].w,
+                                r[6].x, r[6].y, r[6].z, r[6].w, r[7].x, r[7].y, r[7].z, r[7].w};
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 31; i++) acc += w[i] * (uint32_t)__builtin_amdgcn_readlane((int)x, i);
+        x = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readlane((int)x, j);
 }
 
 // mapColumn_: the centre input of column col (1-D, potentialRadius = nin)
@@ -559,13 +592,17 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
             while (rdone < (have >> 8)) convert(rdone++);
             if (have == npd && (npd & 255u) && rdone == (npd >> 8)) convert(rdone++);
         };
+        // the checkpoint (state and the block's undelivered draws) in one load
+        // per lane, read across the lanes afterwards (a load per word made 31
+        // dependent round trips)
+        const uint32_t ckst = l < 31u ? ck[l] : 0u, ckpd = l < 31u ? ck[32 + l] : 0u;
         // the checkpoint block's undelivered draws, one by one (lane 0 writes)
         for (uint32_t j = pend; j < 31u && i < npd; j++) {
-            const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[32 + j]);
             if (sk) {
                 sk--;
                 continue;
             }
+            const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)ckpd, (int)j);
             if (l == 0) lb[i & 511u] = d;
             i++;
         }
@@ -573,7 +610,11 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
         // whole blocks to skip: the scalar generator
         uint32_t st[31];
 #pragma unroll
-        for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[j]);
+        for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readlane((int)ckst, j);
+        if (c.jump && sk >= 31u && i < npd) {
+            sp_jump_blocks(st, sk / 31u, c.jump);
+            sk %= 31u;
+        }
         while (sk >= 31u && i < npd) {
 #pragma unroll
             for (int j = 0; j < 31; j++) st[(3 + j) % 31] += st[j];
