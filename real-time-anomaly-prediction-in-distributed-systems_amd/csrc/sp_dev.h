@@ -665,14 +665,20 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
         return ++i == npd;
     };
     // draws the checkpoint's block had generated but not handed out yet
+    // (the checkpoint in one load per lane, read across the lanes)
+    const uint32_t ckst = l < 31u ? ck[l] : 0u, ckpd = l < 31u ? ck[32 + l] : 0u;
     bool done = false;
-    for (uint32_t j = pend; j < 31u && !done; j++) done = take((uint32_t)__builtin_amdgcn_readfirstlane((int)ck[32 + j]));
+    for (uint32_t j = pend; j < 31u && !done; j++) done = take((uint32_t)__builtin_amdgcn_readlane((int)ckpd, (int)j));
     uint32_t st[31];
 #pragma unroll
-    for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck[j]);
+    for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readlane((int)ckst, j);
 #ifdef HTM_STAMPS
     bool gen_ = false;
 #endif
+    if (c.jump && sk >= 31u && !done) {
+        sp_jump_blocks(st, sk / 31u, c.jump);
+        sk %= 31u;
+    }
     while (!done) {
         if (sk >= 31u) {
 #pragma unroll
