@@ -322,54 +322,76 @@ def pmc_kernel(path, base):
     return ks[0] if ks else None
 
 
-def bench_config5(args, rt, d, world, rank, local):
-    """Config 5 (BASELINE.json configs[4]): the Models 2/3 encoder -- cpu + mem
-    ScalarEncoders (ML/HTM/NetworkUtils.py:89-107, 1000 input bits) -- into a
-    4096-column SP + Model-1 TM, trained on the GPU over the reference's
-    training records (cpu, mem), replicated to every stream, learning off.
-    The timed region replays test records the ModelTesting.py way (each
-    record fed 1 + 7 times, :66-72) and, per record, runs AnomalyLikelihood on
-    the record's score (parity unpinned: NuPIC's likelihood, not in the
-    reference) and the SLO harness on the record's 8-score window
-    (ModelTesting.py:75-146, threshold 0.98, avg-response SLO 70 ms); N>1 GPUs
-    gather every record's likelihoods to rank 0 over RCCL.  `value` counts
-    network stream-steps (8 per record)."""
-    import torch
-    import torch.distributed as dist
-    W = 8
-    nf, ncol = 2, 4096
-    dev = f"cuda:{local}"
-    tr = np.stack([d["train_cpu"], d["train_mem"]], axis=1)
-    train_vals = tr[~np.isnan(tr).any(axis=1)][:2184]
-    S = args.streams
-    n_total = S * world
-    s0, s1 = rt.fleet.shard_range(n_total, world, rank)
-    eng, train_s, hdr, _ = trained_engine(rt, S, args.seg_capacity, local, train_vals, world=world, n_fields=nf,
-                                          sp_columns=ncol)
-    eng.set_learning(False, False)
-    n_rec = (args.warmup + args.steps) // W
-    warm_rec = args.warmup // W
-    # per-record inputs: cpu and mem test traces shifted by 97 s, each with
-    # its own PCG64(724) jitter; mean response time / violations shifted alike
+# config 5's aggregate fields (StreamEngine/StreamAggregator.py:100-115: cpu %,
+# mem %, mean and max response time in ms) in the MultiEncoder's sorted field
+# order, each a ScalarEncoder (n 500, w 21, clipped) over its own range
+FIELDS5 = (("cpu", 0.0, 100.0), ("max", 0.0, 5000.0), ("mean", 0.0, 2000.0), ("mem", 0.0, 100.0))
+C5_KERNEL = "htm_run_frozen_spl_kernel"  # config 5's test phase: SP learning on, TM frozen, run chunks
+
+
+def config5_inputs(d, n_total, s0, s1, n_rec):
+    """Per-record aggregates [n_rec, S, 4] (FIELDS5 order): the reference's
+    TestingData aggregate traces (cpu, max, mean, mem) shifted by 97 s per
+    stream, cpu and mem with PCG64(724) jitter in {-2..2}, the response
+    times scaled by a per-stream factor in [0.9, 1.1]; plus the record's mean
+    response time and violation count (the SLO harness's labels)."""
     rng = np.random.Generator(np.random.PCG64(724))
     t_ = np.arange(n_rec)[:, None]
     g_ = np.arange(s0, s1)[None, :]
     idx = (t_ + 97 * g_) % len(d["test_cpu"])
     jit = rng.integers(-2, 3, size=(2, n_rec, n_total))[:, :, s0:s1]
-    rec = np.stack([np.clip(d["test_cpu"][idx] + jit[0], 0, 100), np.clip(d["test_mem"][idx] + jit[1], 0, 100)],
-                   axis=2).astype(np.float64)  # [n_rec, S, 2]
+    scale = rng.uniform(0.9, 1.1, size=n_total)[None, s0:s1]
+    mean = np.round(d["test_mean"][idx] * scale)
+    rec = np.stack([np.clip(d["test_cpu"][idx] + jit[0], 0, 100), np.round(d["test_max"][idx] * scale), mean,
+                    np.clip(d["test_mem"][idx] + jit[1], 0, 100)], axis=2).astype(np.float64)
+    return rec, mean.astype(np.int32), d["test_violations"][idx].astype(np.int32)
+
+
+def config5_train_values(d):
+    """The reference's training aggregates (FIELDS5 order), records with a
+    null field skipped (ModelTraining.py:29-32), the first 2,184."""
+    tr = np.stack([d["train_cpu"], d["train_max"].astype(np.float64), d["train_mean"].astype(np.float64),
+                   d["train_mem"]], axis=1)
+    return tr[~np.isnan(tr).any(axis=1)][:2184]
+
+
+def run_config5(args, rt, d, world, rank, local, S, warm_rec, n_rec, pmc_summary=None, pmc_note=None):
+    """Config 5 (BASELINE.json configs[4]): the Models 2/3 multi-field shape at
+    its stated size -- the four aggregate fields (FIELDS5) into a 4096-column SP
+    + 12-cell TM, trained on the GPU over the reference's training aggregates
+    (one stream, SP+TM learning on), replicated to every stream; then the
+    ModelTesting.py test phase (:66-72 -> NetworkModel.py:40-44: SP learning
+    on, TM learning off, each record fed 1 + 7 times) and, per record,
+    AnomalyLikelihood on the record's score (parity unpinned: NuPIC's
+    likelihood, not in the reference) and the SLO harness on its 8-score
+    window (ModelTesting.py:75-146, threshold 0.98, avg-response SLO 70 ms).
+    N>1 GPUs: streams sharded, every record's likelihoods gathered to rank 0
+    over RCCL.  `value` counts network stream-steps (8 per record)."""
+    import torch
+    import torch.distributed as dist
+    W = 8
+    dev = f"cuda:{local}"
+    n_total = S * world
+    s0, s1 = rt.fleet.shard_range(n_total, world, rank)
+    mins = tuple(f[1] for f in FIELDS5)
+    maxs = tuple(f[2] for f in FIELDS5)
+    eng, train_s, hdr, _ = trained_engine(rt, S, args.c5_seg_capacity, local, config5_train_values(d), world=world,
+                                          n_fields=4, sp_columns=4096, field_minval=mins, field_maxval=maxs)
+    eng.set_learning(True, False)
+    rec, means_np, viol_np = config5_inputs(d, n_total, s0, s1, warm_rec + n_rec)
     rec_t = torch.tensor(rec, device=dev)
-    vals = rec_t.repeat_interleave(W, dim=0)  # [n_rec * 8, S, 2]: 1 + 7 steps per record
-    means = torch.tensor(d["test_mean"][idx].astype(np.int32), device=dev)
-    viol = torch.tensor(d["test_violations"][idx].astype(np.int32), device=dev)
-    scores = torch.empty((n_rec * W, S), dtype=torch.float32, device=dev)
+    vals = rec_t.repeat_interleave(W, dim=0)  # [records * 8, S, 4]: 1 + 7 steps per record
+    means = torch.tensor(means_np, device=dev)
+    viol = torch.tensor(viol_np, device=dev)
+    scores = torch.empty((vals.shape[0], S), dtype=torch.float32, device=dev)
     lik = rt.harness.AnomalyLikelihood(S, device=local)
     slo = rt.harness.SLOHarness(S, threshold=0.98, device=local)
-    liks = torch.empty((n_rec, S), dtype=torch.float64, device=dev)
+    liks = torch.empty((warm_rec + n_rec, S), dtype=torch.float64, device=dev)
     gather = rt.fleet.ScoreGather(n_total) if world > 1 else None
-    gathered = (torch.empty((n_rec, world, gather.width), dtype=torch.float64, device=dev)
+    gathered = (torch.empty((warm_rec + n_rec, world, gather.width), dtype=torch.float64, device=dev)
                 if world > 1 and rank == 0 else None)
-    chunk_rec = max(1, args.chunk // W)
+    chunk_rec = max(1, args.c5_chunk // W)
+    eng.set_run_chunk(chunk_rec * W)
 
     def replay(r0, r1, handles):
         for a in range(r0, r1, chunk_rec):
@@ -395,7 +417,7 @@ def bench_config5(args, rt, d, world, rank, local):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     handles = []
-    replay(warm_rec, n_rec, handles)
+    replay(warm_rec, warm_rec + n_rec, handles)
     for h in handles:
         h.wait()
     torch.cuda.synchronize()
@@ -406,33 +428,49 @@ def bench_config5(args, rt, d, world, rank, local):
     eng.profile(False)
     c1 = eng.counters()
     if c1["error"]:
-        raise RuntimeError(f"engine overflow flags {c1['error']}")
+        raise RuntimeError(f"config-5 engine overflow flags {c1['error']}")
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    steps = (n_rec - warm_rec) * W
+    steps = n_rec * W
     roof = None
     if prof is not None and prof["tm_ms"] > 0:
-        tm_bytes = c1["tm_bytes"] - c0["tm_bytes"]
+        # the fused kernel's own count of what it moves (frozen-index blocks,
+        # records, state) plus the SP learning terms per
+        # stream-step, over the HIP-event time of its launches
         launches = prof["launches"]
+        per_launch = ((c1["tm_bytes"] - c0["tm_bytes"]) / launches
+                      + sp_learn_bytes(eng) * S * prof["steps"] / launches)
         avg_ms = prof["tm_ms"] / launches
-        achieved = tm_bytes / launches / (avg_ms * 1e-3) / 1e9
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9
+        traffic, k = None, None
+        if pmc_summary:
+            k = pmc_kernel(pmc_summary, C5_KERNEL)
+            traffic = int(k["hbm_bytes_per_dispatch"]) if k and "hbm_bytes_per_dispatch" in k else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "traffic_source": None,
-                "kernel": "htm_run_kernel<false,true> (fused SP+TM, 4096 columns, 2 fields)",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
+                "traffic_source": (f"rocprofv3 --pmc passes of the config-5 workload ({pmc_summary}): "
+                                   f"{k.get('formula', '')}" if traffic else pmc_note),
+                "kernel": C5_KERNEL + " (fused SP+TM run chunks: 4096 columns, 4 fields, SP learning on)",
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
-                "bytes_per_launch": int(tm_bytes / launches), "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4)}
+                "bytes_per_launch": int(per_launch), "issue": issue_record(k)}
     st = slo.stats()
     out = {
-        "metric": METRIC, "value": round(n_total * steps / dt, 1), "unit": "stream-steps/s", "n_gpus": world,
+        "value": round(n_total * steps / dt, 1), "unit": "stream-steps/s",
+        "predictions_per_s": round(n_total * n_rec / dt, 1),
         "steps": steps, "warmup": warm_rec * W, "ms_per_step": round(dt / steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f32+f64",
-        "data": "synthetic: TestingData cpu/mem traces + PCG64(724) jitter, resident in HBM (BASELINE config 5)",
-        "config": {"workload": "config5: cpu+mem encoders (1000 bits), 4096-col SP + 12-cell TM from the GPU-trained "
-                               "state, learn off; per record 1+7 steps + AnomalyLikelihood + SLO harness (0.98)",
-                   "mode": "run", "streams_per_gpu": S, "total_streams": n_total, "columns": ncol,
-                   "cells_per_column": 12, "fields": nf, "records": n_rec - warm_rec,
+        "dtype": "int32+f32+f64",
+        "data": "synthetic: the reference's TestingData aggregates (cpu, max, mean, mem) shifted per stream, "
+                "PCG64(724) jitter, resident in HBM",
+        "config": {"workload": "config5: cpu/max/mean/mem ScalarEncoders (2000 bits, per-field ranges) -> 4096-col SP "
+                               "+ 12-cell TM from the GPU-trained state; the test phase (SP learn on, TM off), per "
+                               "record 1+7 steps + AnomalyLikelihood + SLO harness (0.98)",
+                   "fields": [f[0] for f in FIELDS5], "field_ranges": [[f[1], f[2]] for f in FIELDS5],
+                   "mode": f"run chunks of {chunk_rec} records ({chunk_rec * W} steps), then per record the "
+                           "likelihood and SLO kernels", "streams_per_gpu": S, "total_streams": n_total,
+                   "columns": 4096, "cells_per_column": 12, "records": n_rec,
                    "trained_segments": int(hdr.seg_live), "train_s": round(train_s, 2),
                    "parallelism": f"streams sharded over {world} GPU(s)" +
                                   (", RCCL gather of likelihoods" if world > 1 else "")},
@@ -440,13 +478,107 @@ def bench_config5(args, rt, d, world, rank, local):
         "tm_counters": {k: c1[k] - c0[k] for k in ["inf_phase2", "inf_backtracks"]},
         "slo_totals": {k: int(v) for k, v in zip(["TP", "FP", "TN", "FN", "lead_sum"], st.sum(axis=0))},
     }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     lik.close()
     slo.close()
     eng.close()
+    return out
+
+
+def bench_config5(args, rt, d, world, rank, local):
+    """bench.py --config 5: the config-5 workload (run_config5) as the line."""
+    out = run_config5(args, rt, d, world, rank, local, args.streams, args.warmup // 8, args.steps // 8,
+                      args.pmc_summary)
+    line = {"metric": METRIC, "value": out.pop("value"), "unit": out.pop("unit"), "n_gpus": world,
+            "steps": out.pop("steps"), "warmup": out.pop("warmup"), "ms_per_step": out.pop("ms_per_step"),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None}
+    line.update(out)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def bench_single_stream(rt, src, trace, local, n_rec=256, warm_rec=16):
+    """One Model-1 stream at the reference's own granularity: a prediction is
+    one test record -- ModelTesting.py:66-72 feeds it 1 + 7 times
+    (runNetwork, NetworkModel.py:35-44: SP learning on, TM learning off) and
+    compares the eight scores on the host (:75-79).  The stream is the
+    GPU-trained Model-1 state (`src` stream 0).  Timed per record, the scores
+    copied to the host each record (the alarm decision): `lockstep_steps`
+    (eight htm_step launches per record), `run_chunk` (the record's eight steps
+    as one htm_run launch), and `facade` -- the reference's whole call pattern
+    through the drop-in Network (tests/reference_model1.py: setData, run(1),
+    getOutputData('anomalyScore')[0] eight times, the SDRClassifierRegion
+    running beside it on the GPU).  Beside it the published 20-50 ms per
+    prediction."""
+    import torch
+    dev = f"cuda:{local}"
+    one = rt.HTMEngine(1, device=local, seg_capacity=72 * 1024)
+    for region in rt._lib.ST:
+        one.import_state(region, src.export_state(region, 0, 1), s0=0)
+    one.set_learning(True, False)
+    recs = trace[np.arange(warm_rec + n_rec) % len(trace)].astype(np.float64)
+    v = torch.tensor(recs, device=dev)
+    win = torch.empty((8, 1), dtype=torch.float32, device=dev)
+    res = {}
+    for name in ("lockstep_steps", "run_chunk"):
+        for r in range(warm_rec + n_rec):
+            if r == warm_rec:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            if name == "lockstep_steps":
+                for j in range(8):
+                    one.step(v[r:r + 1], out=win[j])
+            else:
+                one.run(v[r:r + 1].expand(8).reshape(8, 1), out=win)
+            host = win.cpu().numpy()  # the host's alarm decision reads the window
+        dt = time.perf_counter() - t0
+        res[name] = {"ms_per_prediction": round(dt / n_rec * 1e3, 4), "records": n_rec,
+                     "predictions_per_s": round(n_rec / dt, 1)}
+    one.close()
+    # the drop-in surface: Model 1 built and trained through the facade
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import reference_model1 as ref
+    d = np.load(os.path.join(ROOT, "tests", "golden", "model1_traces.npz"))
+    ds = rt.BatchRecordStream(["cpu"])
+    net = ref.create_one_level_network(rt, ds, seg_capacity=72 * 1024, device=local)
+    tmr = net.regions[ref.TMR]
+    t0 = time.perf_counter()
+    n_train = 0
+    for cpu in d["train_cpu"]:
+        if np.isnan(cpu):
+            continue
+        ds.setData(float(cpu))
+        net.run(1)
+        n_train += 1
+        if n_train == 2184:
+            break
+    train_s = time.perf_counter() - t0
+    f_rec = min(n_rec, 128)
+    for r in range(warm_rec + f_rec):
+        if r == warm_rec:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        w = []
+        for j in range(8):
+            ds.setData(float(recs[r]))
+            if j == 0:
+                tmr.setParameter("learningMode", False)  # NetworkModel.py:40-44
+            net.run(1)
+            w.append(tmr.getOutputData("anomalyScore")[0])
+    dt = time.perf_counter() - t0
+    res["facade"] = {"ms_per_prediction": round(dt / f_rec * 1e3, 4), "records": f_rec,
+                     "predictions_per_s": round(f_rec / dt, 1), "train_records": n_train,
+                     "train_ms_per_record": round(train_s / n_train * 1e3, 4),
+                     "note": "Network facade + SDRClassifierRegion (steps 1..7) on the GPU, one stream"}
+    del net
+    res["workload"] = ("config 1 at its own granularity: one Model-1 stream (GPU-trained state), ModelTesting's "
+                       "test phase, a prediction = one record = 1 + 7 network.run(1) steps (SP learn on, TM off) "
+                       "and the eight scores read on the host")
+    res["reference_published"] = {"ms_per_prediction": "20-50", "hardware": "AWS t2.large (2 vCPU), NuPIC 1.0.x",
+                                  "source": "CSC 724 Final Project Report p.8 (SURVEY.md §6)"}
+    return res
 
 
 def main():
@@ -514,15 +646,22 @@ def main():
                          "reference's test phase, NetworkModel.py:40-44)")
     ap.add_argument("--test-phase-steps", type=int, default=256, help="test_phase: timed lockstep steps")
     ap.add_argument("--test-phase-warmup", type=int, default=16, help="test_phase: untimed steps")
-    ap.add_argument("--flush-mode", choices=["auto", "0", "1", "2"], default="auto",
+    ap.add_argument("--no-config5", action="store_true",
+                    help="config 2: skip the config5 sub-record (BASELINE configs[4] on this GPU's shard)")
+    ap.add_argument("--c5-streams", type=int, default=1024, help="config5 sub-record: streams per GPU")
+    ap.add_argument("--c5-records", type=int, default=64, help="config5 sub-record: timed test records (8 steps each)")
+    ap.add_argument("--c5-warmup-records", type=int, default=8, help="config5 sub-record: untimed test records")
+    ap.add_argument("--c5-chunk", type=int, default=256, help="config 5: steps per htm_run chunk")
+    ap.add_argument("--c5-seg-capacity", type=int, default=128 * 1024, help="config 5: segment slots per stream")
+    ap.add_argument("--pmc-summary-c5", default=None, help="counter summary of the config5 leg (see --pmc-summary)")
+    ap.add_argument("--no-single-stream", action="store_true",
+                    help="config 2: skip the single_stream sub-record (one Model-1 stream, ms per prediction)")
+    ap.add_argument("--flush-mode", choices=["auto", "0", "1"], default="auto",
                     help="where the deferred-write flush runs (HTM_OPT_FLUSH_MODE): 0 beside the steps on the "
                          "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
     ap.add_argument("--flush-every", type=int, default=0,
                     help="HTM_OPT_FLUSH_EVERY: lockstep steps between the periodic deferred-write flushes (0: the "
                          "engine default, 8)")
-    ap.add_argument("--wide", type=int, default=0,
-                    help="HTM_OPT_WIDE: up to N of an ordered launch's heaviest TM steps by 768-thread workgroups "
-                         "beside the 256-thread launch (0: off); results identical")
     ap.add_argument("--ordered", choices=["on", "off"], default="on",
                     help="HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first (on, the engine "
                          "default) or one fused SP+TM workgroup per stream in stream order (off); results identical")
@@ -538,8 +677,11 @@ def main():
     if c5:
         args.steps = 2048 if args.steps is None else args.steps
         args.warmup = 64 if args.warmup is None else args.warmup
-        args.streams = 1024 if args.streams is None else args.streams
-        args.seg_capacity = 128 * 1024 if args.seg_capacity is None else args.seg_capacity
+        args.streams = args.c5_streams if args.streams is None else args.streams
+        if args.seg_capacity is not None:
+            args.c5_seg_capacity = args.seg_capacity
+        if args.chunk is not None:
+            args.c5_chunk = args.chunk
     if args.steps is None:
         args.steps = 240 if c3 else 256 if c4 else 2324
     if args.warmup is None:
@@ -569,8 +711,9 @@ def main():
     if standin:
         args.no_learn_on = args.no_cpu = args.no_pmc = args.no_profile = True
     learn_on = args.config == 2 and not args.no_learn_on and args.shape == "model1"
-    pmc_note = pmc_note_learn = None
-    if (int(world_env or "1") == 1 and not args.no_pmc and not c5
+    config5 = args.config == 2 and not args.no_config5 and args.shape == "model1" and not standin
+    pmc_note = pmc_note_learn = pmc_note_c5 = None
+    if (int(world_env or "1") == 1 and not args.no_pmc
             and not os.environ.get("HTM_BENCH_PMC_CHILD")):
         # before this process touches the GPU: the HBM counter passes, each a
         # short run of this same command under rocprofv3 in a child process
@@ -578,6 +721,8 @@ def main():
             args.pmc_summary, pmc_note = self_pmc_passes(args)
         if learn_on and not args.pmc_summary_learn:
             args.pmc_summary_learn, pmc_note_learn = self_pmc_passes(args, learn_leg=True)
+        if config5 and not args.pmc_summary_c5:
+            args.pmc_summary_c5, pmc_note_c5 = self_pmc_passes(args, c5_leg=True)
 
     import torch
     import torch.distributed as dist
@@ -634,6 +779,13 @@ def main():
         eng, train_s, hdr, model_dist = trained_engine(rt, S, args.seg_capacity, local, train_vals, world=world,
                                                        **shape)
         eng.set_learning(False, False)
+    single = (args.config == 2 and args.shape == "model1" and not args.no_single_stream and not standin
+              and rank == 0)
+    if single:
+        # the GPU-trained Model-1 state, for the single-stream record after the headline
+        single_src = rt.HTMEngine(1, device=local, seg_capacity=args.seg_capacity)
+        for region in rt._lib.ST:
+            single_src.import_state(region, eng.export_state(region, 0, 1), s0=0)
     if not c3:
         eng.set_run_chunk(args.chunk)  # one fused launch per htm_run call
     if args.flush_mode != "auto" and not standin:
@@ -642,8 +794,6 @@ def main():
         eng.set_run_unit(args.run_unit)
     if args.ordered == "off" and not standin:
         eng.ordered_steps(False)
-    if args.wide and not standin:
-        eng.wide_steps(args.wide)
     if args.flush_every and not standin:
         eng.flush_every(args.flush_every)
     C = args.condition
@@ -781,7 +931,7 @@ def main():
                                if ordered else "")
                             if args.mode == "step" else
                             "run: htm_run replay chunks, each stream steps through a chunk without waiting"),
-                   "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered, "wide": args.wide,
+                   "conditioning_steps": C, "flush_mode": args.flush_mode, "ordered": args.ordered,
                    "flush_every": args.flush_every,
                    "streams_per_gpu": S, "total_streams": n_total, "columns": eng.n_columns,
                    "cells_per_column": eng.cells_per_column,
@@ -802,6 +952,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and not c3 and not c4 and args.shape == "model1":
         out["cpu_baseline"] = cpu_baseline(trace, train_vals, n_total)
     eng.close()
+    if single:
+        out["single_stream"] = bench_single_stream(rt, single_src, trace, local)
+        single_src.close()
+    if config5:
+        out["config5"] = run_config5(args, rt, d, world, rank, local, args.c5_streams, args.c5_warmup_records,
+                                     args.c5_records, args.pmc_summary_c5, pmc_note_c5)
     if learn_on:
         out["learn_on"] = bench_learn_on(args, rt, trace, world, rank, local, args.pmc_summary_learn, pmc_note_learn)
     if rank == 0:
@@ -846,7 +1002,7 @@ def issue_record(k):
     return rec
 
 
-def self_pmc_passes(args, steps=128, learn_leg=False):
+def self_pmc_passes(args, steps=128, learn_leg=False, c5_leg=False):
     """Run this benchmark's workload (same config/streams, `steps` timed steps,
     the same launch shape as the timed region) under rocprofv3 once per
     counter pass and summarise them (tools/pmc_summary.py); learn_leg: the
@@ -864,6 +1020,12 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
         child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "3", "--steps", str(args.learn_steps),
                  "--warmup", str(args.learn_warmup), "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", "step",
                  "--streams", str(args.learn_streams), "--split-learn", args.split_learn]
+    elif c5_leg or args.config == 5:
+        recs, warm = (args.c5_records, args.c5_warmup_records) if c5_leg else (args.steps // 8, args.warmup // 8)
+        child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "5", "--steps", str(8 * recs),
+                 "--warmup", str(8 * warm), "--no-profile", "--no-pmc", "--streams",
+                 str(args.c5_streams if c5_leg else args.streams), "--c5-chunk", str(args.c5_chunk),
+                 "--c5-seg-capacity", str(args.c5_seg_capacity)]
     else:
         child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
                  "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode,
@@ -872,8 +1034,6 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
             child += ["--flush-mode", args.flush_mode]
         if args.ordered != "on":
             child += ["--ordered", args.ordered]
-        if args.wide:
-            child += ["--wide", str(args.wide)]
         if args.flush_every:
             child += ["--flush-every", str(args.flush_every)]
         for k in ("streams", "seg_capacity", "chunk", "run_unit", "sp_perm_rows", "condition"):
@@ -884,7 +1044,10 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
     passes = dict(PMC_PASSES)
     if args.config == 4 and not learn_leg:
         passes.update(PMC_L2_PASS)  # the fleet's shared model is read from L2: its hit rate
-    passes.update(PMC_SQ_PASSES)
+    if c5_leg:
+        passes.update({"pmc_sq1": PMC_SQ_PASSES["pmc_sq1"]})  # (one SQ pass: issue / wait fractions)
+    else:
+        passes.update(PMC_SQ_PASSES)
     for name, counters in passes.items():
         t0 = time.time()
         cc = list(child)
@@ -906,7 +1069,8 @@ def self_pmc_passes(args, steps=128, learn_leg=False):
     keep = os.environ.get("HTM_BENCH_PMC_KEEP")  # a directory to keep a copy of the summary in
     if keep:
         os.makedirs(keep, exist_ok=True)
-        shutil.copy(path, os.path.join(keep, "pmc_summary_%s.json" % ("learn_on" if learn_leg else "config%d" % args.config)))
+        shutil.copy(path, os.path.join(keep, "pmc_summary_%s.json" % (
+            "learn_on" if learn_leg else "config5" if c5_leg else "config%d" % args.config)))
     return path, None
 
 

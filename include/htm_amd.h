@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define HTM_ABI_VERSION 5
+#define HTM_ABI_VERSION 6
 
 /* error codes */
 #define HTM_OK 0
@@ -177,10 +177,11 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    save, learning on, htm_status / htm_counters, htm_flush.  Results and
                                    state are those of the undeferred step.  0: count every phase 2 in full */
 #define HTM_OPT_FLUSH_MODE 11   /* where the deferred-write flush runs: 0 on the engine's own HIP stream
-                                   beside the next steps, 1 on the step stream after them (full width),
-                                   2 in the tail workgroups of the next ordered launch (other launches as 0).
+                                   beside the next steps, 1 on the step stream after them (full width).
                                    Results are identical; the default is chosen by measurement from the
-                                   engine size (deferred dutyCycle() writes) */
+                                   engine size (deferred dutyCycle() writes).  (ABI 5's mode 2,
+                                   a flush in the tail of the next ordered launch, measured slower and
+                                   was removed in ABI 6) */
 #define HTM_OPT_ORDERED 12      /* 1 (default): a frozen lockstep step (htm_step) of a dense-SP engine of
                                    at most 16,384 streams runs the SP kernel, lists the streams by the
                                    cost of their TM step (the active cells phase 1 will list), and runs
@@ -194,9 +195,8 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    learning included) and then the TM learning kernel with the SP compiled out
                                    (each at its own occupancy); results are identical.  0: one fused SP+TM
                                    learning kernel */
-#define HTM_OPT_WIDE 15         /* ordered frozen lockstep steps: 0 (default) every TM step by a 256-thread
-                                   workgroup; N > 0: up to N of the heaviest steps (the top cost buckets)
-                                   by 768-thread workgroups in a launch beside the others; results identical */
+/* 15: retired in ABI 6 (HTM_OPT_WIDE: the heaviest ordered steps by 768-thread workgroups, measured
+   slower); setting it returns HTM_E_INVALID */
 int htm_set_option(htm_engine* eng, int32_t opt, int32_t value);
 
 /* Complete the deferred dutyCycle() writes (HTM_OPT_DEFER_DUTY): work enqueued

@@ -50,7 +50,6 @@ OPT_FLUSH_MODE = 11
 OPT_ORDERED = 12
 OPT_FLUSH_EVERY = 13
 OPT_SPLIT_LEARN = 14
-OPT_WIDE = 15
 
 
 class HtmConfig(ctypes.Structure):

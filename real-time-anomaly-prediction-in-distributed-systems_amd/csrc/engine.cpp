@@ -64,8 +64,6 @@ struct Region {
 // (profiles/r04_ab/flush_wg.txt)
 #define FLUSH_EVERY 8
 #define FLUSH_WG 768
-#define TAIL_WG 256
-#define WIDE_Q 48  // heavy: a cost estimate >= 3/4 of max_act_cells
 
 struct htm_engine {
     htm_config cfg;
@@ -106,23 +104,13 @@ struct htm_engine {
     hipEvent_t ev_logged = nullptr;   // step stream: the snapshot of the log counters
     hipEvent_t ev_flushed = nullptr;  // fstream: the last enqueued flush is complete
     bool flush_pending = false;       // ev_flushed not yet waited for by a step stream or the host
-    int32_t flush_mode = 0;           // 0: flush stream beside the steps; 1: on the step stream;
-                                      // 2: in the tail of ordered launches (others as 0)
-    int32_t tail_wg = TAIL_WG;        // flush mode 2: tail workers per ordered launch
-    uint32_t tail_launch = 0;         // flush mode 2: ordered launches with a tail (job buffer rotation)
-    bool tail_live = false;           // flush mode 2: a tail launch ran since the last full flush
+    int32_t flush_mode = 0;           // 0: flush stream beside the steps; 1: on the step stream
     int32_t flush_wg = FLUSH_WG;      // grid of a flush beside the steps
     int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
     bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
     int32_t ordered = 1;              // HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first
     int32_t split_learn = 1;          // HTM_OPT_SPLIT_LEARN: learning lockstep steps run the SP kernel, then TM-only
-    int32_t wide = 0;                 // HTM_OPT_WIDE: heavy TM steps of ordered launches by wide workgroups (max)
-    int32_t wide_q = WIDE_Q;          // ... the cost buckets (of ORD_NB) counted heavy: >= wide_q
-    hipStream_t wstream = nullptr;    // the wide launch's stream
-    hipEvent_t ev_sorted = nullptr;   // step stream: the SP kernel (the cost estimates) is done
-    hipEvent_t ev_wide = nullptr;     // wstream: the wide launch is done
-    uint32_t* ord_nh = nullptr;       // [1] heavy streams of the launch (ord_sort_kernel)
     uint32_t* ord = nullptr;          // [n] the ordered launch's stream of each workgroup
     uint16_t* ord_est = nullptr;      // [n] each stream's TM cost estimate (sp_step_ord_kernel)
     unsigned long long* wg_trace = nullptr;  // A/B builds: HTM_WG_TRACE timeline of the latest lockstep launch
@@ -566,9 +554,6 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (n_streams > 16384) e->flush_mode = 1;
     if (const char* env = ab_knob("HTM_FLUSH_MODE")) e->flush_mode = std::atoi(env);                 // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
-    if (const char* env = ab_knob("HTM_WIDE")) e->wide = std::max(0, std::min(1024, std::atoi(env)));  // A/B knob
-    if (const char* env = ab_knob("HTM_WIDE_Q")) e->wide_q = std::max(0, std::min(ORD_NB - 1, std::atoi(env)));  // A/B knob
-    if (const char* env = ab_knob("HTM_TAIL_WG")) e->tail_wg = std::min(FX_FLUSH_WG, std::max(1, std::atoi(env)));  // A/B knob
     if (const char* env = ab_knob("HTM_ORDERED")) e->ordered = std::atoi(env) ? 1 : 0;               // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
@@ -653,9 +638,6 @@ int htm_destroy(htm_engine* e) {
     if (e->ev_logged) (void)hipEventDestroy(e->ev_logged);
     if (e->ev_flushed) (void)hipEventDestroy(e->ev_flushed);
     if (e->fstream) (void)hipStreamDestroy(e->fstream);
-    if (e->ev_sorted) (void)hipEventDestroy(e->ev_sorted);
-    if (e->ev_wide) (void)hipEventDestroy(e->ev_wide);
-    if (e->wstream) (void)hipStreamDestroy(e->wstream);
     delete e;
     return HTM_OK;
 }
@@ -705,18 +687,13 @@ int htm_set_option(htm_engine* e, int32_t opt, int32_t value) {
         e->defer = value ? 1 : 0;
     }
     else if (opt == HTM_OPT_FLUSH_MODE) {
-        if (value < 0 || value > 2)
-            return htm_fail(HTM_E_INVALID, "flush mode must be 0 (beside the steps), 1 (on the step stream) or 2 "
-                            "(in the tail of ordered launches)");
+        if (value < 0 || value > 1)
+            return htm_fail(HTM_E_INVALID, "flush mode must be 0 (beside the steps) or 1 (on the step stream)");
         if (int r = flush_sync(e)) return r;
         e->flush_mode = value;
     }
     else if (opt == HTM_OPT_ORDERED) e->ordered = value ? 1 : 0;
     else if (opt == HTM_OPT_SPLIT_LEARN) e->split_learn = value ? 1 : 0;
-    else if (opt == HTM_OPT_WIDE) {
-        if (value < 0 || value > 1024) return htm_fail(HTM_E_INVALID, "wide: 0 (off) or 1..1024 heavy streams");
-        e->wide = value;
-    }
     else if (opt == HTM_OPT_FLUSH_EVERY) {
         if (value < 0) return htm_fail(HTM_E_INVALID, "flush cadence: 0 (default) or N >= 1 lockstep steps");
         if (int r = flush_sync(e)) return r;
@@ -764,7 +741,6 @@ static int alloc_dlog(htm_engine* e) {
     ALLOC(e->tm.fx_dupto, uint32_t, S);
     ALLOC(e->tm.fx_fq, uint32_t, (size_t)FX_FLUSH_WG * (size_t)d.q_cap);
     ALLOC(e->tm.fx_fwork, uint32_t, FX_FWORK_WORDS);
-    ALLOC(e->tm.fx_tjob, uint4, 3 * S);
     // a split job's id is (stream * fx_dcap + slot) * (fx_nwin + 1) + window (uint32)
     if (S * (size_t)d.fx_dcap * ((size_t)d.fx_nwin + 1) >= ((size_t)1 << 32))
         return htm_fail(HTM_E_CAPACITY, "deferred-write flush: %zu streams x %d ring slots x %d windows overflow the "
@@ -795,7 +771,6 @@ static int flush_async(htm_engine* e, hipStream_t st) {
         if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1, 0))
             return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
         e->defer_steps = 0;
-        e->tail_live = false;
         return HTM_OK;
     }
     if (launch_tm_fx_snap(e->tm, e->n, st)) return htm_fail(HTM_E_HIP, "flush snapshot launch");
@@ -823,7 +798,6 @@ static int flush_deferred(htm_engine* e, hipStream_t st) {
     if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1, 1))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     e->defer_steps = 0;
-    e->tail_live = false;  // (its done kernel voids the published tail jobs)
     return HTM_OK;
 }
 
@@ -853,8 +827,6 @@ static int build_fx(htm_engine* e, hipStream_t st) {
         HIP_TRY(hipMemsetAsync(e->tm.fx_dflushed, 0, (size_t)e->n * 4, st));
         HIP_TRY(hipMemsetAsync(e->tm.fx_dsnap, 0, (size_t)e->n * 4, st));
         HIP_TRY(hipMemsetAsync(e->tm.fx_dupto, 0, (size_t)e->n * 4, st));
-        HIP_TRY(hipMemsetAsync(e->tm.fx_fwork + FX_TCNT, 0, (FX_FWORK_WORDS - FX_TCNT) * 4, st));
-        e->tail_live = false;
     }
     if (launch_tm_fx_rank(d, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "fx rank launch");
     if (launch_tm_fx_count(d, e->tm, e->d_counts, e->nm, st)) return htm_fail(HTM_E_HIP, "fx count launch");
@@ -990,31 +962,13 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     if (int r = encode_rdse(e, d_values, n_steps, st)) return r;
     // deferred dutyCycle() writes: frozen lockstep launches (one step)
     const bool defer = frozen && n_steps == 1 && e->defer;
-    // flush mode 2: an ordered launch replays the entries the previous one
-    // published in its own tail; the two schemes never overlap -- a flush
-    // beside the steps is waited for before a tail launch, and the tail jobs
-    // are flushed (voided) before a deferring launch of the other kind
-    const bool tail = defer && ordered && e->flush_mode == 2;
     TmBufs tb = e->tm;
     if (defer) {
         if (int r = alloc_dlog(e)) return r;
-        if (tail && e->flush_pending) {
-            HIP_TRY(hipStreamWaitEvent(st, e->ev_flushed, 0));
-            e->flush_pending = false;
-        }
-        if (!tail && e->tail_live) {
-            if (int r = flush_deferred(e, st)) return r;
-        }
         tb = e->tm;
-        if (tail) {
-            tb.fx_tail_wg = e->tail_wg;
-            tb.fx_tpar = e->tail_launch++ % 3u;
-            e->tail_live = true;
-        }
     } else {
         tb.fx_dlog = nullptr;
     }
-    const bool wide = ordered && e->wide > 0;
     if (ordered) {
         if (!e->ord) {
             ALLOC(e->ord, uint32_t, e->n);
@@ -1024,33 +978,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
             return htm_fail(HTM_E_HIP, "sp_step launch");
         tb.ord = e->ord;
         tb.tm_only = 1;
-        if (wide) {
-            if (!e->ord_nh) {
-                ALLOC(e->ord_nh, uint32_t, 1);
-                int least = 0, greatest = 0;
-                HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-                HIP_TRY(hipStreamCreateWithPriority(&e->wstream, hipStreamNonBlocking, greatest));
-                HIP_TRY(hipEventCreateWithFlags(&e->ev_sorted, hipEventDisableTiming));
-                HIP_TRY(hipEventCreateWithFlags(&e->ev_wide, hipEventDisableTiming));
-            }
-            // the heavy steps: the wide kernel picks them from the SP kernel's
-            // estimates and starts beside ord_sort_kernel (one workgroup), on
-            // the idle chip, ahead of the 256-thread launch; the step stream
-            // joins it after that launch
-            TmBufs tw = tb;
-            tw.ord_role = 1;  // (a wide workgroup is never a tail worker: grid <= n)
-            tw.ord_est = e->ord_est;
-            tw.wide_q = e->wide_q;
-            tw.wide_max = e->wide;
-            HIP_TRY(hipEventRecord(e->ev_sorted, st));
-            HIP_TRY(hipStreamWaitEvent(e->wstream, e->ev_sorted, 0));
-            if (launch_htm_run_wide(e->dc, tw, e->sp, d_values, d_scores, e->n, std::min(e->wide, e->n), e->wstream))
-                return htm_fail(HTM_E_HIP, "wide launch: %s", hipGetErrorString(hipGetLastError()));
-            HIP_TRY(hipEventRecord(e->ev_wide, e->wstream));
-            tb.ord_nh = e->ord_nh;
-            tb.ord_role = 2;
-        }
-        if (launch_ord_sort(e->dc, e->ord_est, e->ord, e->n, st, e->wide_q, e->wide, wide ? e->ord_nh : nullptr))
+        if (launch_ord_sort(e->dc, e->ord_est, e->ord, e->n, st))
             return htm_fail(HTM_E_HIP, "ord_sort launch");
         if (prof) HIP_TRY(hipEventRecord(ev[1], st));  // (the 256-thread TM launch's start)
     } else if (split) {
@@ -1074,12 +1002,10 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     if (launch_htm_run(e->dc, tb, e->sp, d_values, d_scores, n_steps, e->sp_learn, e->tm_learn, frozen,
                        e->keep_prev, e->keep_overlaps, e->n, e->wq, unit, st))
         return htm_fail(HTM_E_HIP, "htm_run launch: %s", hipGetErrorString(hipGetLastError()));
-    if (wide) HIP_TRY(hipStreamWaitEvent(st, e->ev_wide, 0));
     e->conf_packed = true;
     if (prof) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
     // (an explicit cadence, HTM_OPT_FLUSH_EVERY, is taken as given: past the ring the log fills)
-    if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : std::min(FLUSH_EVERY, e->dc.fx_dcap / 2)) &&
-        !tail) {
+    if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : std::min(FLUSH_EVERY, e->dc.fx_dcap / 2))) {
         int r = flush_async(e, st);  // beside the next steps
         if (r) return r;
     }

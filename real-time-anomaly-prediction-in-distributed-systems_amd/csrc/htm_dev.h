@@ -224,33 +224,10 @@ struct TmBufs {
     // instead of wherever the stream order puts them.
     const uint32_t* ord;           // [S] stream of each workgroup (null: workgroup b runs stream b)
     int32_t tm_only;               // 1: the launch skips the SP (ordered launches)
-    // Wide heavy streams (ordered launches, HTM_OPT_WIDE): the first wide_max
-    // streams (stream order) whose cost bucket is >= wide_q run on the wide
-    // kernel (HTM_WIDE_NT threads), which picks them itself from the SP
-    // kernel's estimates -- so it starts beside ord_sort_kernel, before the
-    // 256-thread launch fills the CUs; ord_sort_kernel lists the other n - h
-    // (h = *ord_nh) for the 256-thread launch.
-    const uint32_t* ord_nh;        // [1] h (device)
-    int32_t ord_role;              // 0: workgroup b runs ord[b]; 1 (wide): wide_stream(b); 2: ord[b] for b < n - h
-    const uint16_t* ord_est;       // [S] the SP kernel's cost estimates (the wide kernel's selection)
-    int32_t wide_q, wide_max;      // heavy: bucket >= wide_q; at most wide_max streams
-    // Tail flush (ordered frozen lockstep launches, HTM_OPT_FLUSH_MODE 2): the
-    // launch's workgroups past the n stream workgroups replay the deferred-log
-    // entries the previous tail launch's steps published -- in the launch's
-    // tail, where stream workgroups are draining, instead of a flush beside the
-    // next steps.  Job buffers rotate over three launches: launch L's steps
-    // publish into buffer L % 3, its tail workers replay buffer (L + 2) % 3,
-    // and its first tail worker clears buffer (L + 1) % 3 for launch L + 1.
-    uint4* fx_tjob;                // [3][S] {stream, first entry, end entry, 0}
-    int32_t fx_tail_wg;            // tail workers in this launch (0: no tail flush)
-    uint32_t fx_tpar;              // L % 3
 };
-// fx_fwork words of the tail flush: job counts of the three buffers, claim counters
-#define FX_TCNT 4
-#define FX_TCLAIM 7
-#define FX_FWORK_WORDS 10
+#define FX_FWORK_WORDS 4
 #define ORD_NB 64                  // cost buckets of the ordering (active-cell estimate / (max_act_cells / 64))
-// the cost bucket of an active-cell estimate (ord_sort_kernel, wide_stream)
+// the cost bucket of an active-cell estimate (ord_sort_kernel)
 __host__ __device__ inline uint32_t ord_bucket(uint32_t est, uint32_t mac) {
     const uint32_t q = (uint32_t)(((unsigned long long)est * 64u) / (mac + 1u));
     return q < 64u ? q : 63u;
@@ -551,12 +528,7 @@ int launch_tm_fx_count(const DevCfg& c, const TmBufs& b, uint64_t* counts, int n
 int launch_tm_fx_fill(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_fx_flush(const DevCfg& c, const TmBufs& b, int n, int max_wg, hipStream_t st, int from_dn, int split);
 int launch_tm_fx_snap(const TmBufs& b, int n, hipStream_t st);
-// ord_sort also counts the streams in cost buckets >= heavy_q (at most heavy_max) into *nh
-int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st, int heavy_q = 0,
-                    int heavy_max = 0, uint32_t* nh = nullptr);
-// the wide kernel for ordered launches' heavy streams (tm_k_wide.hip)
-int launch_htm_run_wide(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values, float* scores,
-                        int n, int grid, hipStream_t st);
+int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st);
 int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                        const uint32_t* tm_bm, uint16_t* est, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

@@ -612,8 +612,11 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
 #pragma unroll
         for (int j = 0; j < 31; j++) st[j] = (uint32_t)__builtin_amdgcn_readlane((int)ckst, j);
         if (c.jump && sk >= 31u && i < npd) {
-            sp_jump_blocks(st, sk / 31u, c.jump);
-            sk %= 31u;
+            // the tables cover skips below 2^SP_JUMP_POW blocks; the scalar
+            // loop below takes any remainder
+            const uint32_t nj = (sk / 31u) & ((1u << SP_JUMP_POW) - 1u);
+            sp_jump_blocks(st, nj, c.jump);
+            sk -= 31u * nj;
         }
         while (sk >= 31u && i < npd) {
 #pragma unroll
@@ -676,8 +679,9 @@ static __device__ __forceinline__ void sp_regen_row(SpInitCfg c_, int s_, int co
     bool gen_ = false;
 #endif
     if (c.jump && sk >= 31u && !done) {
-        sp_jump_blocks(st, sk / 31u, c.jump);
-        sk %= 31u;
+        const uint32_t nj = (sk / 31u) & ((1u << SP_JUMP_POW) - 1u);  // (the loop takes any remainder)
+        sp_jump_blocks(st, nj, c.jump);
+        sk -= 31u * nj;
     }
     while (!done) {
         if (sk >= 31u) {
@@ -913,6 +917,7 @@ __device__ __forceinline__ void sp_adapt_wave(const DevCfg& c, const SpBufs& b, 
 #pragma unroll
                 for (int k = 0; k < 8; k++) pv[k] = (uint32_t)k < pc ? sf[r0 + k] : 0.0f;
                 const uint32_t cw = col >> 5, cb = 1u << (col & 31);
+                float* sfw = reinterpret_cast<float*>(scratch);
                 uint32_t x = byte;
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
@@ -926,9 +931,25 @@ __device__ __forceinline__ void sp_adapt_wave(const DevCfg& c, const SpBufs& b, 
                         else p = p + c.sp_below_inc;
                         bool newc;
                         p = sp_update_perm(c, p, mode == 0, newc);
-                        row[r0 + k] = p;
+                        sfw[r0 + k] = p;  // (in place: each lane rewrites its own ranks)
                         if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
                     }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                // the row written back from the scratch with each store
+                // instruction covering one contiguous run: float4 q = lane +
+                // 64 i (1 KiB per instruction, whole 128-byte lines of a pool
+                // row -- its padding past n_potential gets the staged zeros;
+                // per-rank 4-byte stores left 64-byte partial-line writes,
+                // 1.5x the row's bytes, profiles/r05_end); scalar runs when
+                // the row is not 16-byte aligned (dense rows, npot % 4 != 0)
+                if (vec) {
+                    const int n4 = paged ? c.pool_stride >> 2 : npot >> 2;
+                    float4* row4 = reinterpret_cast<float4*>(row);
+                    for (int q = l; q < n4; q += 64) row4[q] = st4[q];
+                } else {
+                    for (int q = l; q < npot; q += 64) row[q] = sfw[q];
                 }
                 __builtin_amdgcn_wave_barrier();  // (the scratch is restaged next)
             }

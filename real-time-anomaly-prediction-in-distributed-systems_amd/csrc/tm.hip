@@ -48,8 +48,7 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     const void* fn = which == 0 ? tmk_fn_run_learn() : which == 1 ? tmk_fn_run_frozen()
                      : which == 2 ? tmk_fn_run_frozen_paged() : which == 4 ? tmk_fn_run_frozen_spl()
                      : which == 5 ? tmk_fn_run_learn_tm() : tmk_fn_run_infer();
-    // (a frozen lockstep launch may carry tail flush workers past the streams)
-    const int grid = nblk == 1 ? total + (frozen && b.fx_tail_wg > 0 ? b.fx_tail_wg : 0) : run_grid(fn, lds, total);
+    const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
     switch (which) {
         case 0: return tmk_launch_run_learn(grid, lds, st, HTM_RUN_PASS);
         case 1: return tmk_launch_run_frozen(grid, lds, st, HTM_RUN_PASS);
@@ -333,11 +332,6 @@ int tm_configure_lds(const DevCfg& c) {
     int r = tmk_attr_step(b0, b1, b2);
     r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1) |
          tmk_attr_run_frozen_spl(b1) | tmk_attr_run_learn_tm(b0);
-#ifdef HTM_WIDE_LDS_MIN
-    r |= tmk_attr_run_wide(std::max(tmk_wide_lds_bytes(c), (size_t)HTM_WIDE_LDS_MIN));
-#else
-    r |= tmk_attr_run_wide(tmk_wide_lds_bytes(c));
-#endif
     r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
                  hipSuccess ? 0 : -1;
     (void)hipGetLastError();
@@ -403,37 +397,14 @@ __global__ __launch_bounds__(TM_NT) void tm_fx_flush_kernel(DevCfg c, TmBufs b, 
 // first: a counting sort over ORD_NB cost buckets by one workgroup (streams
 // within a bucket in no particular order -- streams are independent, so the
 // order never changes a result).
-__global__ __launch_bounds__(1024) void ord_sort_kernel(DevCfg c, const uint16_t* est, uint32_t* ord, int n,
-                                                        int heavy_q, int heavy_max, uint32_t* nh) {
-    __shared__ uint32_t hist[ORD_NB], at[ORD_NB], wsum[16];
-    extern __shared__ uint8_t bkt[];  // [n] bucket of each stream (0xFF: the wide launch's)
+__global__ __launch_bounds__(1024) void ord_sort_kernel(DevCfg c, const uint16_t* est, uint32_t* ord, int n) {
+    __shared__ uint32_t hist[ORD_NB], at[ORD_NB];
+    extern __shared__ uint8_t bkt[];  // [n] bucket of each stream
     const uint32_t mac = (uint32_t)c.max_act_cells;
     for (int q = threadIdx.x; q < ORD_NB; q += blockDim.x) hist[q] = 0;
     for (int s = threadIdx.x; s < n; s += blockDim.x) bkt[s] = (uint8_t)ord_bucket(est[s], mac);
     __syncthreads();
-    if (nh) {
-        // wide launch (HTM_OPT_WIDE): the first heavy_max streams, in stream
-        // order, of the buckets >= heavy_q go to the wide kernel, which picks
-        // the same ones (wide_stream); the rest are ordered here
-        const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
-        const int s0 = (int)threadIdx.x * per;
-        uint32_t cnt = 0;
-        for (int k = 0; k < per; k++) cnt += (s0 + k < n && bkt[s0 + k] >= heavy_q) ? 1u : 0u;
-        const uint32_t incl = wave_incl_scan(cnt);
-        if (lane_id() == 63) wsum[threadIdx.x >> 6] = incl;
-        __syncthreads();
-        uint32_t r = incl - cnt, tot = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
-            if (w < (int)(threadIdx.x >> 6)) r += wsum[w];
-            tot += wsum[w];
-        }
-        for (int k = 0; k < per && s0 + k < n; k++)
-            if (bkt[s0 + k] >= heavy_q && r++ < (uint32_t)heavy_max) bkt[s0 + k] = 0xFF;
-        if (threadIdx.x == 0) *nh = tot < (uint32_t)heavy_max ? tot : (uint32_t)heavy_max;
-        __syncthreads();
-    }
-    for (int s = threadIdx.x; s < n; s += blockDim.x)
-        if (bkt[s] != 0xFF) atomicAdd(&hist[bkt[s]], 1u);
+    for (int s = threadIdx.x; s < n; s += blockDim.x) atomicAdd(&hist[bkt[s]], 1u);
     __syncthreads();
     static_assert(ORD_NB == 64, "one lane per bucket");
     if (threadIdx.x < 64) {  // exclusive prefix, heaviest bucket first (lane l: bucket 63 - l)
@@ -441,15 +412,12 @@ __global__ __launch_bounds__(1024) void ord_sort_kernel(DevCfg c, const uint16_t
         at[63 - threadIdx.x] = wave_incl_scan(h) - h;
     }
     __syncthreads();
-    for (int s = threadIdx.x; s < n; s += blockDim.x)
-        if (bkt[s] != 0xFF) ord[atomicAdd(&at[bkt[s]], 1u)] = (uint32_t)s;
+    for (int s = threadIdx.x; s < n; s += blockDim.x) ord[atomicAdd(&at[bkt[s]], 1u)] = (uint32_t)s;
 }
 
-int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st, int heavy_q,
-                    int heavy_max, uint32_t* nh) {
+int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, hipStream_t st) {
     if (n <= 0 || n > ORD_MAX_STREAMS) return -1;  // (n + 512 bytes of LDS)
-    if (nh && (heavy_q < 0 || heavy_q >= ORD_NB || heavy_max < 0)) return -1;
-    hipLaunchKernelGGL(ord_sort_kernel, dim3(1), dim3(1024), (size_t)n, st, c, est, ord, n, heavy_q, heavy_max, nh);
+    hipLaunchKernelGGL(ord_sort_kernel, dim3(1), dim3(1024), (size_t)n, st, c, est, ord, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -502,9 +470,6 @@ __global__ void tm_fx_flush_done_kernel(TmBufs b, int n) {
         b.fx_fwork[0] = 0u;
         b.fx_fwork[2] = 0u;
     }
-    // every entry up to fx_dupto is flushed: the tail flush's published jobs
-    // (ordered launches) are void
-    if (s < FX_FWORK_WORDS - FX_TCNT) b.fx_fwork[FX_TCNT + s] = 0u;
 }
 
 // the entries a flush enqueued now covers (on the step stream, after the steps)

@@ -2539,17 +2539,29 @@ __device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA
     return inSeq;
 }
 
-// _learnPhase2(readOnly)
-__device__ __forceinline__ void learn_phase2(Tm& t, bool ro) {
+// _learnPhase2(readOnly).  A read-only pass of a learn backtrack (`next`: the
+// columns of the pattern after it) computes lrnPredictedState only for those
+// columns: its one reader is the next pattern's read-only _learnPhase1, which
+// looks at the next pattern's columns alone (learn_backtrack_from); every
+// pass that writes recomputes lrnP in full before anything else reads it.
+// The best-match search then reads the rows of those columns' segments only
+// (scan_best's flagged form) instead of the whole pool.
+__device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* next = nullptr, int nnext = 0) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int K = c.K;
     if (threadIdx.x == 0) sh->st[2]++;
     wg_clear(t.lrnP, c.cw);
     wg_clear(t.U, 2 * c.ncol);
+    const bool part = ro && next != nullptr;
+    if (part) {
+        wg_clear(t.flags, c.nw);
+        __syncthreads();
+        for (int a = threadIdx.x; a < nnext; a += TM_NT) atomicOr(&t.flags[next[a] >> 5], 1u << (next[a] & 31));
+    }
     __syncthreads();
     STAMP(t, SB_LEARN);
-    scan_best(t, t.lrnA, c.act_thr, nullptr);
+    scan_best(t, t.lrnA, c.act_thr, part ? t.flags : nullptr);
     __syncthreads();
     STAMP(t, SB_LSCAN);
     const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
@@ -2695,7 +2707,12 @@ __device__ __forceinline__ bool learn_backtrack_from(Tm& t, int start, bool ro) 
             inSeq = learn_phase1(t, pat, len, ro);
         }
         if (!inSeq || off == cur) break;
+#ifdef HTM_LP2_FULL_RO  // (A/B builds: read-only passes over every column)
         learn_phase2(t, ro);
+#else
+        if (ro) learn_phase2(t, true, lrn_pat(t, off + 1), lrn_len(t, off + 1));
+        else learn_phase2(t, false);
+#endif
     }
     return inSeq;
 }
@@ -2927,7 +2944,7 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
 // active cells, the counting of rank window `win` (-1: every window), the
 // qualifying segments' first dutyCycle() record writes (phase2_duty_only).
 // The calling workgroup's qualifying list is fx_fq's row `worker`.  Used by
-// tm_fx_flush_kernel and by the tail workers of ordered launches.
+// tm_fx_flush_kernel.
 __device__ __forceinline__ void fx_replay_entry(const DevCfg& c, const TmBufs& b, int s, uint32_t i, uint32_t len,
                                                 int win, uint32_t worker, uint8_t* lds) {
     Tm t;
@@ -2957,89 +2974,6 @@ __device__ __forceinline__ void fx_replay_entry(const DevCfg& c, const TmBufs& b
     }
     __syncthreads();
     phase2_duty_only(t);
-}
-
-// A tail worker of an ordered frozen launch (TmBufs::fx_tjob): claims the
-// jobs the previous tail launch's steps published -- one per stream, the
-// entries [first, end) of its ring -- replays them, and marks them flushed
-// (fx_dflushed only grows: atomicMax).  The workers start once every stream
-// workgroup is dispatched, so they fill the slots the draining steps free.
-// Worker 0 first clears the buffer the next launch publishes into.
-__device__ __forceinline__ void fx_tail_worker(const DevCfg& c, const TmBufs& b, int n, uint8_t* lds) {
-    __shared__ uint32_t job_sh;
-    const uint32_t worker = blockIdx.x - (uint32_t)n;
-    const uint32_t par = b.fx_tpar, rd = (par + 2u) % 3u, nx = (par + 1u) % 3u;
-    const uint32_t dcap = (uint32_t)c.fx_dcap;
-    if (worker == 0 && threadIdx.x == 0) {
-        b.fx_fwork[FX_TCNT + nx] = 0u;
-        b.fx_fwork[FX_TCLAIM + nx] = 0u;
-    }
-    uint32_t total = b.fx_fwork[FX_TCNT + rd];
-    total = total < (uint32_t)c.n_streams ? total : (uint32_t)c.n_streams;
-    const uint4* jobs = b.fx_tjob + (size_t)rd * (uint32_t)c.n_streams;
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) job_sh = atomicAdd(&b.fx_fwork[FX_TCLAIM + rd], 1u);
-        __syncthreads();
-        const uint32_t j = __builtin_amdgcn_readfirstlane(job_sh);
-        if (j >= total) break;
-        const uint4 jb = jobs[j];
-        const uint32_t su = __builtin_amdgcn_readfirstlane(jb.x), f = __builtin_amdgcn_readfirstlane(jb.y),
-                       u = __builtin_amdgcn_readfirstlane(jb.z);
-        if (su >= (uint32_t)n || u - f > dcap) {
-            if (threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOB);
-            continue;
-        }
-        for (uint32_t e = f; e != u; e++) {
-            const uint32_t i = e % dcap;
-            const uint32_t len = b.fx_dlen[(size_t)su * dcap + i];
-            if (len > (uint32_t)c.max_act_cells) {
-                if (threadIdx.x == 0) atomicOr(&b.fx_fwork[1], FX_ERR_JOB);
-                continue;
-            }
-            fx_replay_entry(c, b, (int)su, i, len, -1, worker, lds);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&b.fx_dflushed[su], u);
-    }
-}
-
-// Stream of wide workgroup b (HTM_OPT_WIDE): the b-th stream, in stream
-// order, whose cost bucket is >= wide_q, if b < wide_max; else -1 -- the same
-// streams ord_sort_kernel leaves out of the 256-thread launch's list.  Every
-// thread returns it.  Contains barriers: call uniformly.
-__device__ __forceinline__ int wide_stream(const DevCfg& c, const TmBufs& b, int n, TmSh* sh, uint32_t blk) {
-    const uint32_t mac = (uint32_t)c.max_act_cells;
-    const int per = (n + TM_NT - 1) / TM_NT;
-    const int s0 = (int)threadIdx.x * per;
-    uint32_t cnt = 0;
-    for (int k = 0; k < per && s0 + k < n; k++) cnt += ord_bucket(b.ord_est[s0 + k], mac) >= (uint32_t)b.wide_q ? 1u : 0u;
-    if (threadIdx.x == 0) sh->ti[0] = -1;
-    uint32_t tot;
-    uint32_t r = wg_excl_scan(sh, cnt, &tot);  // (barriers: ti[0] is set before any thread writes it)
-    if (blk < (uint32_t)b.wide_max && blk >= r && blk < r + cnt) {
-        for (int k = 0; k < per && s0 + k < n; k++)
-            if (ord_bucket(b.ord_est[s0 + k], mac) >= (uint32_t)b.wide_q && r++ == blk) sh->ti[0] = s0 + k;
-    }
-    __syncthreads();
-    const int s = sh->ti[0];
-    __syncthreads();
-    return s;
-}
-
-// The step's side of the tail flush: publish stream s's entries logged since
-// its last publication (fx_dupto: published up to) for the next tail launch.
-// Thread 0 only.
-__device__ __forceinline__ void fx_tail_publish(const DevCfg& c, const TmBufs& b, int s, uint32_t dn) {
-    const uint32_t pu = b.fx_dupto[s];
-    if (dn == pu) return;
-    const uint32_t k = atomicAdd(&b.fx_fwork[FX_TCNT + b.fx_tpar], 1u);
-    if (k < (uint32_t)c.n_streams) {
-        b.fx_tjob[(size_t)b.fx_tpar * (uint32_t)c.n_streams + k] = make_uint4((uint32_t)s, pu, dn, 0u);
-        b.fx_dupto[s] = dn;
-    } else {
-        atomicOr(&b.fx_fwork[1], FX_ERR_JOBS);  // (never: one job per stream)
-    }
 }
 
 // Write the inference state back to HBM without reading anything: the
@@ -3347,10 +3281,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         if (LEARN && (!first || (int)threadIdx.x == sh->ti[1])) hdr->lrn_pat_len[threadIdx.x] = sh->lrn_len[threadIdx.x];
     }
     if (threadIdx.x == 0) {
-        if (t.defer) {
-            b.fx_dn[s] = t.dn;
-            if (b.fx_tail_wg > 0) fx_tail_publish(c, b, s, t.dn);
-        }
+        if (t.defer) b.fx_dn[s] = t.dn;
         hdr->avg_input_density = sh->avg_dens;
         hdr->avg_learned_seq_length = sh->avg_lsl;
         hdr->lrn_iter = sh->lrn_iter;
@@ -3419,7 +3350,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
 #define HTM_SPL_PLANES 1
 #endif
 // NOSP compiles the SP out (TM-only launches: the SP kernel ran first)
-template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true, bool NOSP = false, bool WIDE = false>
+template <bool LEARN, bool FROZEN, bool PAGED_OK, bool SPL = true, bool NOSP = false>
 __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const double* values,
                                              float* scores, int n_steps, int sp_learn, int keep_prev,
                                              int keep_overlaps, uint32_t* wq, int unit_steps, int n) {
@@ -3442,24 +3373,14 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
 #ifdef HTM_AB_KNOBS
     const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (FROZEN && direct && b.fx_tail_wg > 0 && blockIdx.x >= (uint32_t)n) {
-        fx_tail_worker(c, b, n, lds);  // (the launch's tail: the deferred-log flush)
-        return;
-    }
     uint32_t u = 0xFFFFFFFFu;
     int s = 0, k = 0, k0 = 0, k1 = 0;
     for (;;) {
         if (k == k1 && direct) {
             if (u != 0xFFFFFFFFu || blockIdx.x >= (uint32_t)n) break;
             u = blockIdx.x;
-            if constexpr (WIDE) {  // the wide kernel's heavy streams
-                s = wide_stream(c, b, n, reinterpret_cast<TmSh*>(lds), blockIdx.x);
-                if (s < 0) break;
-            } else {
-                if (b.ord_role == 2 && blockIdx.x >= (uint32_t)n - __builtin_amdgcn_readfirstlane(*b.ord_nh)) break;
-                s = b.ord ? (int)__builtin_amdgcn_readfirstlane(b.ord[blockIdx.x]) : (int)blockIdx.x;
-                if (s >= n) break;  // (never: ord lists streams)
-            }
+            s = b.ord ? (int)__builtin_amdgcn_readfirstlane(b.ord[blockIdx.x]) : (int)blockIdx.x;
+            if (s >= n) break;  // (never: ord lists streams)
             k0 = k = 0;
             k1 = n_steps;
         }
@@ -3568,8 +3489,6 @@ TM_RUN_KERNEL_DECL(run_frozen_paged)
 TM_RUN_KERNEL_DECL(run_learn)
 TM_RUN_KERNEL_DECL(run_learn_tm)
 TM_RUN_KERNEL_DECL(run_infer)
-TM_RUN_KERNEL_DECL(run_wide)
-size_t tmk_wide_lds_bytes(const DevCfg& c);
 // unfused TM step kernels (learn, frozen index, pool scan)
 int tmk_launch_step(int learn, int frozen, int grid, size_t lds, hipStream_t st, DevCfg c, TmBufs b, SpBufs sp,
                     float* scores);

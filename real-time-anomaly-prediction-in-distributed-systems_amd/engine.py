@@ -238,8 +238,7 @@ class HTMEngine:
 
     def flush_mode(self, mode: int):
         """Where the deferred-write flush runs: 0 beside the next steps on the
-        engine's own HIP stream, 1 on the step stream, 2 in the tail of the
-        next ordered launch (other launches as 0); results identical."""
+        engine's own HIP stream, 1 on the step stream; results identical."""
         check(self._L.htm_set_option(self.h, _lib.OPT_FLUSH_MODE, int(mode)))
 
     def flush_every(self, steps: int):
@@ -251,12 +250,6 @@ class HTMEngine:
         """Learning lockstep steps run the SP kernel, then the TM-only learning
         kernel (HTM_OPT_SPLIT_LEARN, default on); results are identical."""
         check(self._L.htm_set_option(self.h, _lib.OPT_SPLIT_LEARN, int(on)))
-
-    def wide_steps(self, n: int):
-        """Ordered frozen lockstep steps run up to n of their heaviest TM steps
-        (the top cost buckets) by 768-thread workgroups in a launch beside the
-        256-thread one (HTM_OPT_WIDE; 0 = off); results are identical."""
-        check(self._L.htm_set_option(self.h, _lib.OPT_WIDE, int(n)))
 
     def ordered_steps(self, on: bool):
         """Frozen lockstep steps run their TM steps heaviest first

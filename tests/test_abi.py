@@ -63,7 +63,7 @@ def test_default_config_is_the_reference_model1(rt):
 
 def test_abi_version_and_error_string(rt):
     L = rt._lib.lib()
-    assert L.htm_abi_version() == 5
+    assert L.htm_abi_version() == 6
     assert isinstance(L.htm_last_error(), bytes)
 
 

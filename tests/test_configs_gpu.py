@@ -261,3 +261,74 @@ def test_config5_four_field_aggregate_4096_columns(rt, oracle_mod, traces):
             assert g == o, f"record {k}: gpu {g} oracle {o}"
     sp_equal(eng, 0, orc)
     tm_equal(eng, 0, orc)
+
+
+def test_config5_1024_streams_test_phase_vs_oracle(rt, oracle_mod, traces):
+    """Config 5 at one GPU's shard: 1,024 streams of the bench's four-field
+    aggregate model (bench.FIELDS5 ranges, bench.config5_inputs records: the
+    reference's TestingData cpu/max/mean/mem, StreamAggregator.py:100-115)
+    into 4096 columns.  Fresh streams (seed 2045 + s) learn 48 records
+    (lockstep, SP+TM on), then run the test phase the way bench.run_config5
+    does (ModelTesting.py:66-72: SP learning on, TM off, each record fed 1 + 7
+    times in htm_run chunks, AnomalyLikelihood and the SLO harness per
+    record).  Five sampled streams equal independent oracle models at every
+    step; their likelihoods equal the restatement within 1e-6 relative (parity
+    unpinned w.r.t. NuPIC) and their SLO counts the literal harness exactly.
+    (Fresh streams instead of the bench's trained state keep the oracle's
+    share of the test to seconds.)"""
+    import bench
+    import likelihood_reference as lr
+    from test_slo_harness import gpu_stats, ref_stats
+    n, L, R, W = 1024, 48, 80, 8
+    sampled = (0, 1, 333, 700, n - 1)
+    mins = tuple(f[1] for f in bench.FIELDS5)
+    maxs = tuple(f[2] for f in bench.FIELDS5)
+    d = traces["raw"]
+    rec, means, viol = bench.config5_inputs(d, n, 0, n, L + R)
+    rec[5, 17, 1] = np.nan  # a missing aggregate field (learning phase)
+    rec[L + 3, 333, 2] = np.nan  # ... and in a test record of a sampled stream
+    eng = rt.HTMEngine(n, seed_stride=1, n_fields=4, sp_columns=4096, seg_capacity=1 << 13,
+                       field_minval=mins, field_maxval=maxs)
+    lkp = dict(learning_period=30, estimation_samples=20, historic_window=120, reestimation_period=25)
+    lik = rt.AnomalyLikelihood(n, **lkp)
+    slo = rt.SLOHarness(n, threshold=0.98)
+    v = torch.tensor(rec, device="cuda")
+    idx = torch.tensor(sampled, device="cuda")
+    eng.set_learning(True, True)
+    learn = np.stack([eng.step(v[k]).index_select(0, idx).cpu().numpy() for k in range(L)])
+    eng.set_learning(True, False)
+    eng.set_run_chunk(16 * W)
+    vals = v[L:].repeat_interleave(W, dim=0)
+    scores = torch.empty((R * W, n), dtype=torch.float32, device="cuda")
+    liks = torch.empty((R, n), dtype=torch.float64, device="cuda")
+    mt, vt = torch.tensor(means[L:], device="cuda"), torch.tensor(viol[L:], device="cuda")
+    for a in range(0, R, 16):
+        eng.run(vals[a * W:(a + 16) * W], out=scores[a * W:(a + 16) * W])
+        for r in range(a, a + 16):
+            lik.anomaly_probability(v[L + r], scores[r * W], out=liks[r])
+            slo.record(scores[r * W:(r + 1) * W], vt[r], mt[r])
+    eng.status()
+    got = scores.index_select(1, idx).cpu().numpy().reshape(R, W, len(sampled))
+    got_lik = liks.index_select(1, idx).cpu().numpy()
+    stats = slo.stats()
+    orcs = []
+    for s in sampled:
+        p = oracle_mod.default_params(sp_seed=2045 + s, tm_seed=2045 + s, n_fields=4, sp_columns=4096)
+        for f in range(4):
+            p.field_minval[f], p.field_maxval[f] = mins[f], maxs[f]
+        orcs.append(oracle_mod.OracleModel(p))
+    for k in range(L):
+        for i, (s, o) in enumerate(zip(sampled, orcs)):
+            assert learn[k, i] == o.step(rec[k, s], True, True), f"learning record {k} stream {s}"
+    for i, (s, o) in enumerate(zip(sampled, orcs)):
+        ref = lr.AnomalyLikelihood(lkp["learning_period"], lkp["estimation_samples"], lkp["historic_window"],
+                                   lkp["reestimation_period"])
+        windows = []
+        for r in range(R):
+            win = [o.step(rec[L + r, s], True, False) for _ in range(W)]
+            assert np.array_equal(got[r, :, i], np.array(win, np.float32)), f"test record {r} stream {s}"
+            want_lik = ref.anomaly_probability(rec[L + r, s, 0], float(win[0]))
+            np.testing.assert_allclose(got_lik[r, i], want_lik, rtol=1e-6, atol=0, err_msg=f"record {r} stream {s}")
+            windows.append(win)
+        assert gpu_stats(stats[s]) == ref_stats(windows, means[L:, s], viol[L:, s], 0.98), f"SLO stream {s}"
+    assert np.any(got_lik != 0.5)

@@ -148,44 +148,3 @@ def test_flush_overlapping_snapshots(rt, model1, traces):
     for region in ("tm_seg_duty", "tm_seg_meta"):
         assert np.array_equal(a.export_state(region), b.export_state(region)), region
 
-
-@pytest.mark.parametrize("sp_learn", [False, True])
-def test_tail_flush_equals_undeferred(rt, model1, traces, sp_learn):
-    """Flush mode 2: each ordered launch replays, in its own tail, the entries
-    the previous one published.  Scores, counters and segment records equal
-    the undeferred engine -- through a stretch of unordered steps (the
-    periodic flush beside the steps; the tail jobs are flushed before it), a
-    mid-run export (a full flush) and the end of the run."""
-    n, T = 1536, 72
-    rng = np.random.default_rng(91)
-    test = np.asarray(traces["test"], np.float64)
-    t = np.arange(T)[:, None]
-    s = np.arange(n)[None, :]
-    vals = torch.tensor(np.clip(test[(t + 29 * s) % len(test)] + rng.integers(-2, 3, size=(T, n)), 0, 100),
-                        device="cuda")
-    a = replicas(rt, model1, n)
-    a.flush_mode(2)
-    b = replicas(rt, model1, n)
-    b.defer_duty(False)
-    for e in (a, b):
-        e.set_learning(sp_learn, False)
-    out_a, out_b = [], []
-    for k in range(T):
-        if k == 24:
-            a.ordered_steps(False)  # unordered: deferral with the periodic flush
-        if k == 40:
-            a.ordered_steps(True)
-        if k == 56:
-            assert np.array_equal(a.export_state("tm_seg_duty"), b.export_state("tm_seg_duty"))
-        out_a.append(a.step(vals[k]).cpu().numpy())
-        out_b.append(b.step(vals[k]).cpu().numpy())
-    assert np.array_equal(np.stack(out_a), np.stack(out_b))
-    ca, cb = a.counters(), b.counters()
-    for k in ("inf_phase2", "inf_backtracks", "seg_live", "error"):
-        assert ca[k] == cb[k], k
-    assert ca["error"] == 0 and ca["inf_backtracks"] > 0
-    for region in ("tm_seg_duty", "tm_seg_meta", "tm_bitmaps", "tm_header"):
-        xa, xb = a.export_state(region), b.export_state(region)
-        if region == "tm_header":  # the algorithmic byte counter differs by design
-            xa, xb = xa[:, :-8], xb[:, :-8]
-        assert np.array_equal(xa, xb), region

@@ -64,32 +64,13 @@ def test_ordered_equals_stream_order(rt, model1, traces, n, sp_learn, defer):
         assert np.array_equal(a.export_state(region), b.export_state(region)), region
 
 
-@pytest.mark.parametrize("n,sp_learn,defer,wide", [(1024, False, True, 32), (300, True, True, 1024),
-                                                   (2000, False, False, 64)])
-def test_wide_heavy_steps_equal(rt, model1, traces, n, sp_learn, defer, wide):
-    """HTM_OPT_WIDE: the heaviest TM steps of each ordered launch by 768-thread
-    workgroups beside the 256-thread launch -- scores at every step, counters
-    and the exported state equal the 256-thread-only launch (a wide grid past
-    the stream count included)."""
-    T = 64
-    rng = np.random.default_rng(11 + n)
-    test = np.asarray(traces["test"], np.float64)
-    t = np.arange(T)[:, None]
-    s = np.arange(n)[None, :]
-    vals = torch.tensor(np.clip(test[(t + 41 * s) % len(test)] + rng.integers(-2, 3, size=(T, n)), 0, 100),
-                        device="cuda")
-    a = replicas(rt, model1, n)
-    b = replicas(rt, model1, n)
-    a.wide_steps(wide)
-    for e in (a, b):
-        e.set_learning(sp_learn, False)
-        e.defer_duty(defer)
-        e.flush_mode(1)
-    ga, gb = lockstep(a, vals), lockstep(b, vals)
-    assert np.array_equal(ga, gb)
-    ca, cb = a.counters(), b.counters()
-    for k in ("tm_bytes", "inf_phase2", "inf_backtracks", "seg_live", "error"):
-        assert ca[k] == cb[k], k
-    assert ca["error"] == 0 and ca["inf_backtracks"] > 0
-    for region in ("tm_seg_duty", "tm_bitmaps", "tm_colconf", "tm_header", "sp_perm", "sp_duty"):
-        assert np.array_equal(a.export_state(region), b.export_state(region)), region
+def test_retired_options_are_refused(rt, model1):
+    """ABI 6 removed HTM_OPT_WIDE (15) and flush mode 2 (both measured
+    slower): setting them fails loudly."""
+    e = replicas(rt, model1, 4)
+    with pytest.raises(RuntimeError):
+        e.set_option(15, 1)
+    with pytest.raises(RuntimeError):
+        e.flush_mode(2)
+    e.flush_mode(1)
+    e.flush_mode(0)

@@ -33,8 +33,6 @@ eng, _, _, _ = bench.trained_engine(rt, N, 72 * 1024, 0, train)
 eng.set_learning(False, False)
 if os.environ.get("SH_FLUSH_EVERY"):
     eng.flush_every(int(os.environ["SH_FLUSH_EVERY"]))
-if os.environ.get("SH_WIDE"):
-    eng.wide_steps(int(os.environ["SH_WIDE"]))
 if os.environ.get("SH_FLUSH_MODE"):
     eng.flush_mode(int(os.environ["SH_FLUSH_MODE"]))
 T = COND + WARM + REGIONS * STEPS
