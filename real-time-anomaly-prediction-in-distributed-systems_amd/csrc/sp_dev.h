@@ -931,6 +931,9 @@ __device__ __forceinline__ void sp_adapt_wave(const DevCfg& c, const SpBufs& b, 
                         else p = p + c.sp_below_inc;
                         bool newc;
                         p = sp_update_perm(c, p, mode == 0, newc);
+#ifdef HTM_SP_RANK_STORES  // (A/B builds: the round-5 per-rank stores)
+                        row[r0 + k] = p;
+#endif
                         sfw[r0 + k] = p;  // (in place: each lane rewrites its own ranks)
                         if (oldc != newc) atomicXor(&connT[(size_t)input * c.nw + cw], cb);
                     }
@@ -944,12 +947,18 @@ __device__ __forceinline__ void sp_adapt_wave(const DevCfg& c, const SpBufs& b, 
                 // per-rank 4-byte stores left 64-byte partial-line writes,
                 // 1.5x the row's bytes, profiles/r05_end); scalar runs when
                 // the row is not 16-byte aligned (dense rows, npot % 4 != 0)
+#ifdef HTM_SP_RANK_STORES
+                if (false) {
+#else
                 if (vec) {
+#endif
                     const int n4 = paged ? c.pool_stride >> 2 : npot >> 2;
                     float4* row4 = reinterpret_cast<float4*>(row);
                     for (int q = l; q < n4; q += 64) row4[q] = st4[q];
                 } else {
+#ifndef HTM_SP_RANK_STORES
                     for (int q = l; q < npot; q += 64) row[q] = sfw[q];
+#endif
                 }
                 __builtin_amdgcn_wave_barrier();  // (the scratch is restaged next)
             }
