@@ -878,7 +878,7 @@ def main():
         if args.pmc_summary:
             # HBM bytes per launch measured by rocprofv3 --pmc passes of THIS command
             # (tools/pmc_summary.py, run in the same gpurun call; corrections there)
-            traffic, k = split_traffic(args.pmc_summary, split, kernel_name(c3, c4, eng.fused, split))
+            traffic, k = split_traffic(args.pmc_summary, split, kernel_name(c3, c4, eng.fused, split, ordered))
             if traffic:
                 tsrc = (f"rocprofv3 --pmc passes of this command ({args.pmc_summary}): {k.get('formula', '')}; "
                         "calibrated on tools/fetch_calib (profiles/r02_final/pmc_summary.json)")
@@ -886,7 +886,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
                 "traffic_source": tsrc,
-                "kernel": (f"{SP_LEARN_KERNEL} + " if split else "") + kernel_name(c3, c4, eng.fused, split),
+                "kernel": (f"{SP_LEARN_KERNEL} + " if split else "") + kernel_name(c3, c4, eng.fused, split, ordered),
                 "avg_launch_ms": round(avg_ms, 4), "steps_per_launch": prof["steps"] / launches,
                 "profiled_launches": launches, "bytes_per_launch": int(per_launch), "issue": issue_record(k),
                 "sp_kernel_avg_ms": round(prof["sp_ms"] / launches, 4) if not ordered else None}
@@ -1029,7 +1029,7 @@ def self_pmc_passes(args, steps=128, learn_leg=False, c5_leg=False):
     else:
         child = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(args.config), "--steps", str(steps),
                  "--warmup", "8", "--other-steps", "0", "--no-cpu", "--no-profile", "--no-pmc", "--mode", args.mode,
-                 "--no-learn-on", "--no-test-phase", "--shape", args.shape]
+                 "--no-learn-on", "--no-test-phase", "--no-config5", "--no-single-stream", "--shape", args.shape]
         if args.flush_mode != "auto":
             child += ["--flush-mode", args.flush_mode]
         if args.ordered != "on":
@@ -1077,21 +1077,24 @@ def self_pmc_passes(args, steps=128, learn_leg=False, c5_leg=False):
 SP_LEARN_KERNEL = "sp_step_ord_kernel<true, true>"  # the split learning step's SP kernel (paged permanences)
 
 
-def kernel_name(c3, c4, fused, split=False):
+def kernel_name(c3, c4, fused, split=False, ordered=False):
     """The dominant kernel's name as rocprofv3 reports it (without the
     argument list): the fused SP+TM kernel, frozen-TM or learning variant
-    (split learning steps: the TM-only learning kernel)."""
+    (split learning steps: the TM-only learning kernel; ordered frozen steps:
+    the TM-only frozen kernel)."""
     if not fused:
         return "tm_step_kernel<false, true>" if not c3 else "tm_step_kernel<true, false>"
     if c3:
         return "htm_run_tmlearn_kernel" if split else "htm_run_kernel<true>"
-    return "htm_run_frozen_kernel"
+    return "htm_run_frozen_tm_kernel" if ordered else "htm_run_frozen_kernel"
 
 
 def split_traffic(path, split, tm_kernel):
     """HBM bytes per learning step from the counter passes: the TM kernel's,
     plus the SP kernel's for a split step; (bytes, TM kernel record)."""
     k = pmc_kernel(path, tm_kernel)
+    if not k and tm_kernel == "htm_run_frozen_tm_kernel":  # (A/B builds without the TM-only kernel)
+        k = pmc_kernel(path, "htm_run_frozen_kernel")
     if not k or "hbm_bytes_per_dispatch" not in k:
         return None, k
     b = k["hbm_bytes_per_dispatch"]

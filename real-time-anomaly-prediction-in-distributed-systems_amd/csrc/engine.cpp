@@ -304,13 +304,16 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // qualifying segments ranked in LDS: as many (<= 1024) as the phase-2
     // bucket arrays leave room for in the LDS budget; more go through HBM
     {
+        // (the finish arrays are the learning / pool-scan layouts': sized as at
+        // three frozen workgroups per CU whatever the frozen budget)
+        const size_t qb = std::max(lds_budget, (size_t)52 * 1024);
         const size_t off_u0 = tm_step_lds_base(d, 0, 1);
-        const size_t avail0 = lds_budget > off_u0 ? (lds_budget - off_u0) / 4 : 0;
+        const size_t avail0 = qb > off_u0 ? (qb - off_u0) / 4 : 0;
         const size_t fixed = (size_t)d.ncol + (size_t)(d.ncol + 1) / 2 + (size_t)d.ncol + 1 + (size_t)d.nw;
         size_t q = avail0 > fixed ? (avail0 - fixed) * 2 / 9 : 0;
         q = q / 64 * 64;
         if (q > 1024) q = 1024;
-        if (q < 64) return htm_fail(HTM_E_INVALID, "LDS budget %zu too small for the phase-2 buckets", lds_budget);
+        if (q < 64) return htm_fail(HTM_E_INVALID, "LDS budget %zu too small for the phase-2 buckets", qb);
         d.q_lds = (int32_t)q;
     }
     // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
@@ -355,7 +358,8 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // done): bursting steps (~1,500-2,000 qualifying segments on config 2) stay
     // in LDS instead of taking the HBM-scratch path
     {
-        const size_t uw = (tm_step_lds_bytes(d, 0, 1) - tm_step_lds_base(d, 0, 1)) / 4;
+        // (the TM-only launch's union: no SP words -- the smaller of the two frozen layouts)
+        const size_t uw = (tm_step_lds_bytes(d, 0, 1, 1) - tm_step_lds_base(d, 0, 1)) / 4;
         d.q_lds_fx = (int32_t)(uw * 2 / 3 / 64 * 64);
     }
     return HTM_OK;
@@ -538,6 +542,10 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     // three frozen-inference workgroups per CU (HTM_RUN_WAVES): 160 KiB / 3,
     // less the run kernel's static LDS, rounded down to 1 KiB
     size_t budget = optin >= 54 * 1024 ? (size_t)52 * 1024 : (size_t)optin - 2048;
+#ifdef HTM_TM_LDS_BUDGET_DEFAULT
+    // (experiment builds, e.g. four frozen TM-only workgroups per CU: 40 KiB)
+    budget = std::min(budget, (size_t)HTM_TM_LDS_BUDGET_DEFAULT);
+#endif
     if (const char* env = ab_knob("HTM_TM_LDS_BUDGET")) {  // tuning knob (bytes)
         long v = std::strtol(env, nullptr, 10);
         if (v >= 16384 && v <= optin) budget = (size_t)v;

@@ -533,7 +533,7 @@ int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, i
                        const uint32_t* tm_bm, uint16_t* est, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
-size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen);
+size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen, int nosp = 0);
 size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen);  // offset of the union region
 int tm_configure_lds(const DevCfg& c);
 int launch_prev_pred(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);

@@ -6,7 +6,7 @@
 
 #include "tm_core.h"
 
-size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).total; }
+size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen, int nosp) { return tm_layout(c, learn, frozen, nosp).total; }
 size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen) { return tm_layout(c, learn, frozen).off_U; }
 
 static int run_grid(const void* fn, size_t lds, int total) {
@@ -35,7 +35,8 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
                    uint32_t* wq, int unit_steps, hipStream_t st) {
     if (n <= 0 || n_steps <= 0) return 0;
     if (unit_steps < 1) unit_steps = 1;
-    size_t lds = tm_step_lds_bytes(c, tm_learn, frozen);
+    // (a TM-only launch needs no SP words: its own, smaller, LDS request)
+    size_t lds = tm_step_lds_bytes(c, tm_learn, frozen, b.tm_only ? 1 : 0);
     const long nblk = (n_steps + unit_steps - 1) / unit_steps;
     if ((long)n * nblk >= 0x7FFFFFFFL) return -1;
     const int total = (int)(n * nblk);
@@ -45,13 +46,21 @@ int launch_htm_run(const DevCfg& c, const TmBufs& b, const SpBufs& sp, const dou
     // its learning) needs no SP code: the inference-only frozen kernel
     const int which = tm_learn ? (b.tm_only ? 5 : 0)
                                : frozen ? (c.sp_paged ? 2 : (sp_learn && !b.tm_only) ? 4 : 1) : 3;
-    const void* fn = which == 0 ? tmk_fn_run_learn() : which == 1 ? tmk_fn_run_frozen()
+    // TM-only frozen launches (ordered lockstep steps): the kernel with the SP
+    // compiled out (fewer registers: 153 VGPRs vs 166)
+#ifdef HTM_NO_TMONLY_KERNEL  // (A/B builds: TM-only launches on the fused kernel)
+    const bool tmo = false;
+#else
+    const bool tmo = which == 1 && b.tm_only;
+#endif
+    const void* fn = which == 0 ? tmk_fn_run_learn() : which == 1 ? (tmo ? tmk_fn_run_frozen_tm() : tmk_fn_run_frozen())
                      : which == 2 ? tmk_fn_run_frozen_paged() : which == 4 ? tmk_fn_run_frozen_spl()
                      : which == 5 ? tmk_fn_run_learn_tm() : tmk_fn_run_infer();
     const int grid = nblk == 1 ? total : run_grid(fn, lds, total);
     switch (which) {
         case 0: return tmk_launch_run_learn(grid, lds, st, HTM_RUN_PASS);
-        case 1: return tmk_launch_run_frozen(grid, lds, st, HTM_RUN_PASS);
+        case 1: return tmo ? tmk_launch_run_frozen_tm(grid, lds, st, HTM_RUN_PASS)
+                           : tmk_launch_run_frozen(grid, lds, st, HTM_RUN_PASS);
         case 2: return tmk_launch_run_frozen_paged(grid, lds, st, HTM_RUN_PASS);
         case 4: return tmk_launch_run_frozen_spl(grid, lds, st, HTM_RUN_PASS);
         case 5: return tmk_launch_run_learn_tm(grid, lds, st, HTM_RUN_PASS);
@@ -331,6 +340,7 @@ int tm_configure_lds(const DevCfg& c) {
     size_t b0 = tm_step_lds_bytes(c, 1, 0), b1 = tm_step_lds_bytes(c, 0, 1), b2 = tm_step_lds_bytes(c, 0, 0);
     int r = tmk_attr_step(b0, b1, b2);
     r |= tmk_attr_run_learn(b0) | tmk_attr_run_frozen(b1) | tmk_attr_run_infer(b2) | tmk_attr_run_frozen_paged(b1) |
+         tmk_attr_run_frozen_tm(tm_step_lds_bytes(c, 0, 1, 1)) |
          tmk_attr_run_frozen_spl(b1) | tmk_attr_run_learn_tm(b0);
     r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
                  hipSuccess ? 0 : -1;

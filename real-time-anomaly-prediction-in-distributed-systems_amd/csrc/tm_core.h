@@ -146,7 +146,8 @@ struct TmLayout {
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int frozen) {
+// nosp: a TM-only launch (the SP kernel ran first): no SP step in the union
+__host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int frozen, int nosp = 0) {
     TmLayout L;
     L.nbm = learn ? 7 : 3;
     size_t o = align16(sizeof(TmSh));
@@ -168,15 +169,18 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     //          block prefix u32[max_act_cells+1], list starts u32[max_act_cells],
     //          block -> list map u16[FX_OWN]
     //  trim flags (learning): u32[upd_cap]
-    size_t fin = (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
-                 (size_t)(c.q_lds + 1) / 2 + (size_t)c.nw;
+    //  (the frozen tail is phase2_finish_ranked's, in the frozen collection's
+    //  words: no finish arrays)
+    size_t fin = frozen && !learn ? 0
+                                  : (size_t)c.ncol + (size_t)(c.ncol + 1) / 2 + (size_t)c.ncol + 1 + 4 * (size_t)c.q_lds +
+                                        (size_t)(c.q_lds + 1) / 2 + (size_t)c.nw;
     size_t keys = learn ? 2 * (size_t)c.ncol + LREC_WORDS + ((size_t)c.ncol + 1) / 2 : 0;
     size_t col = frozen ? (size_t)c.fx_win / 4 + 64 + (size_t)(c.max_act_cells + 1) / 2 + 2 * (size_t)c.max_act_cells +
                               1 + FX_OWN / 2
                         : 0;
     size_t trim = learn ? (size_t)c.upd_cap : 0;
     // the fused kernels' SP step, and the boosted-inhibition keys after it
-    size_t spw = align16(sizeof(SpShared)) / 4 + (c.sp_boost != 0.0f ? ((size_t)c.nw + 1) * 32 : 0) + SP_PLANE_WORDS;
+    size_t spw = nosp ? 0 : align16(sizeof(SpShared)) / 4 + (c.sp_boost != 0.0f ? ((size_t)c.nw + 1) * 32 : 0) + SP_PLANE_WORDS;
     size_t u = fin;
     if (spw > u) u = spw;
     if (keys > u) u = keys;
@@ -3484,6 +3488,7 @@ __device__ __forceinline__ void htm_run_body(const DevCfg& c, const TmBufs& b, c
     int tmk_launch_##name(int grid, size_t lds, hipStream_t st, HTM_RUN_ARGS);                       \
     int tmk_attr_##name(size_t lds);
 TM_RUN_KERNEL_DECL(run_frozen)
+TM_RUN_KERNEL_DECL(run_frozen_tm)
 TM_RUN_KERNEL_DECL(run_frozen_spl)
 TM_RUN_KERNEL_DECL(run_frozen_paged)
 TM_RUN_KERNEL_DECL(run_learn)
