@@ -318,7 +318,8 @@ typedef struct {
     uint32_t error;          /* bit 0 seg pool full, bit 1 update queue full */
     uint32_t stat_inf_phase2, stat_inf_backtrack, stat_lrn_phase2, stat_lrn_backtrack;
     uint16_t inf_pat_head, lrn_pat_head; /* ring-buffer heads of the histories */
-    uint32_t pad;
+    uint32_t lp2_pending;    /* engine-internal: the last learning step's final learnPhase2 is deferred
+                                into the next step's first pool scan; always 0 in exported / saved state */
     uint64_t stat_bytes;     /* algorithmic HBM bytes moved by the TM kernel (accumulated) */
 } htm_tm_header;
 

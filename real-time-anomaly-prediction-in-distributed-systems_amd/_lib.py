@@ -98,7 +98,7 @@ class TmHeader(ctypes.Structure):
         ("n_upd", ctypes.c_int32), ("error", ctypes.c_uint32),
         ("stat_inf_phase2", ctypes.c_uint32), ("stat_inf_backtrack", ctypes.c_uint32),
         ("stat_lrn_phase2", ctypes.c_uint32), ("stat_lrn_backtrack", ctypes.c_uint32),
-        ("inf_pat_head", ctypes.c_uint16), ("lrn_pat_head", ctypes.c_uint16), ("pad", ctypes.c_uint32),
+        ("inf_pat_head", ctypes.c_uint16), ("lrn_pat_head", ctypes.c_uint16), ("lp2_pending", ctypes.c_uint32),
         ("stat_bytes", ctypes.c_uint64),
     ]
 

@@ -109,6 +109,7 @@ struct htm_engine {
     int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
     bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
+    bool lp2_pending = false;         // a learning step may have left its final learn phase 2 pending
     int32_t ordered = 1;              // HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first
     int32_t split_learn = 1;          // HTM_OPT_SPLIT_LEARN: learning lockstep steps run the SP kernel, then TM-only
     uint32_t* ord = nullptr;          // [n] the ordered launch's stream of each workgroup
@@ -319,6 +320,12 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
     // measured (profiles/r01_ab): the nonzero-column bitmap beats column buckets (+1.5%) and the
     // bitonic key sort at Model-1 sizes
     d.fin_mode = 2;
+    // learning steps defer their final learn phase 2 into the next step's first
+    // pool scan (tm_core.h lp2_finish): 32-bit keys hold slots < 2^21
+    d.lp2_defer = d.seg_cap <= (1 << 21) ? 1 : 0;
+#ifdef HTM_NO_LP2_DEFER  // (A/B builds)
+    d.lp2_defer = 0;
+#endif
     if (const char* env = ab_knob("HTM_TM_FIN"))
         d.fin_mode = std::strcmp(env, "sorted") == 0 ? 1 : std::strcmp(env, "buckets") == 0 ? 0 : 2;
     // frozen-inference counter window: the union region holds the u8
@@ -812,7 +819,20 @@ static int flush_deferred(htm_engine* e, hipStream_t st) {
 // Host-side flush before the host reads or replaces the state: every stream
 // of the device is drained first (the steps may have been issued on any
 // stream, e.g. torch's current one), then the flush runs to completion.
+// Complete the learning steps' pending final learn phase 2s (enqueued on st).
+static int finish_lp2(htm_engine* e, hipStream_t st) {
+    if (!e->lp2_pending) return HTM_OK;
+    if (launch_tm_lp2_finish(e->dc, e->tm, e->nm, st)) return htm_fail(HTM_E_HIP, "lp2 finish launch");
+    e->lp2_pending = false;
+    return HTM_OK;
+}
+
 static int flush_sync(htm_engine* e) {
+    if (e->lp2_pending) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (int r = finish_lp2(e, nullptr)) return r;
+        HIP_TRY(hipDeviceSynchronize());
+    }
     if (!e->tm.fx_dlog) return HTM_OK;
     HIP_TRY(hipDeviceSynchronize());
     if (e->defer_steps) {
@@ -892,6 +912,12 @@ static int next_events(htm_engine* e, hipEvent_t* ev, int32_t steps) {
 // with TM learning off the frozen forward index is (re)built first.
 static int prepare_step(htm_engine* e, hipStream_t st, int* frozen) {
     *frozen = 0;
+    // a step without TM learning completes what the last learning step deferred
+    if (!e->tm_learn && e->lp2_pending) {
+        int r = finish_lp2(e, st);
+        if (r) return r;
+    }
+    if (e->tm_learn && e->dc.lp2_defer) e->lp2_pending = true;
     if (e->tm_learn || !e->use_frozen) {
         // the pool scans read the segments' dutyCycle records
         int r = flush_deferred(e, st);
@@ -1471,6 +1497,7 @@ int htm_import_state(htm_engine* e, int32_t region, int32_t s0, int32_t n, const
 
 int htm_reset_tm(htm_engine* e, void* stream) {
     if (!e) return htm_fail(HTM_E_INVALID, "null engine");
+    if (int r = finish_lp2(e, (hipStream_t)stream)) return r;  // (the deferred phase precedes the reset)
     if (launch_tm_reset(e->dc, e->tm, e->n, (hipStream_t)stream)) return htm_fail(HTM_E_HIP, "reset launch");
     return invalidate_colnz(e, stream);
 }

@@ -70,6 +70,7 @@ struct DevCfg {
     int32_t q_lds;                        // qualifying segments sorted in LDS (more: global path)
     int32_t q_lds_fx;                     // ... of a frozen phase 2 ranked in LDS (column u16 + dutyCycle f32
                                           // in the whole union region; more: the HBM scratch)
+    int32_t lp2_defer;                    // learning steps defer their final learnPhase2 (tm_core.h lp2_finish)
     int32_t fin_mode;                     // phase-2 tail: 0 column buckets (scans over all columns),
                                           // 1 bitonic key sort, 2 buckets over the nonzero-column bitmap
     int32_t max_act_cells;                // num_desired * K (frozen collection cell list)
@@ -532,6 +533,7 @@ int launch_ord_sort(const DevCfg& c, const uint16_t* est, uint32_t* ord, int n, 
 int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, int learn, int n, int keep_overlaps,
                        const uint32_t* tm_bm, uint16_t* est, hipStream_t st);
 int launch_tm_reset(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
+int launch_tm_lp2_finish(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 int launch_tm_compact(const DevCfg& c, const TmBufs& b, int n, hipStream_t st);
 size_t tm_step_lds_bytes(const DevCfg& c, int learn, int frozen, int nosp = 0);
 size_t tm_step_lds_base(const DevCfg& c, int learn, int frozen);  // offset of the union region

@@ -93,6 +93,58 @@ int launch_tm_init(const DevCfg& c, const TmBufs& b, const uint64_t* seeds, int 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Complete the pending final learn phase 2 of every stream whose last
+// learning step deferred it (htm_tm_header::lp2_pending; tm_core.h
+// lp2_finish): lrnPredictedState, the queued updates and the generator, as
+// the step itself would have left them.  One workgroup per stream; streams
+// with nothing pending return at once.
+__global__ __launch_bounds__(TM_NT) void tm_lp2_finish_kernel(DevCfg c, TmBufs b) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int s = blockIdx.x;
+    htm_tm_header* hdr = b.hdr + s;
+    if (__builtin_amdgcn_readfirstlane(hdr->lp2_pending) == 0u) return;
+    Tm t;
+    tm_bind<true, false>(t, c, b, s, s, lds);
+    TmSh* sh = t.sh;
+    uint32_t* gbm = b.bm + (size_t)s * 4 * c.cw;
+    if (threadIdx.x == 0) {
+        sh->lrn_iter = hdr->lrn_iter;
+        sh->rf = hdr->rng_f;
+        sh->rr = hdr->rng_r;
+        sh->hwm = hdr->seg_hwm;
+        sh->nlive = hdr->seg_live;
+        sh->n_upd = hdr->n_upd;
+        sh->err = hdr->error;
+        sh->st[2] = hdr->stat_lrn_phase2;
+        sh->lp2p = 1;
+        sh->lp2s = 0;
+        sh->bytes = 0;
+    }
+    if (threadIdx.x < 31) sh->rng[threadIdx.x] = hdr->rng_state[threadIdx.x];
+    for (int w = threadIdx.x; w < c.cw; w += TM_NT) t.lrnA1[w] = gbm[2 * c.cw + w];  // lrnActiveState of that step
+    __syncthreads();
+    lp2_finish(t, sh->lrn_iter);
+    for (int w = threadIdx.x; w < c.cw; w += TM_NT) gbm[3 * c.cw + w] = t.lrnP1[w];
+    if (threadIdx.x < 31) hdr->rng_state[threadIdx.x] = sh->rng[threadIdx.x];
+    if (threadIdx.x == 0) {
+        hdr->rng_f = sh->rf;
+        hdr->rng_r = sh->rr;
+        hdr->seg_hwm = sh->hwm;
+        hdr->seg_live = sh->nlive;
+        hdr->n_upd = sh->n_upd;
+        hdr->error = sh->err;
+        hdr->stat_lrn_phase2 = sh->st[2];
+        hdr->stat_bytes += sh->bytes;
+        hdr->lp2_pending = 0u;
+    }
+}
+
+int launch_tm_lp2_finish(const DevCfg& c, const TmBufs& b, int n, hipStream_t st) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(tm_lp2_finish_kernel, dim3(n), dim3(TM_NT), tm_step_lds_bytes(c, 1, 0), st, c, b);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // BacktrackingTM.reset(): clears t and t-1 states (colConfidence is kept),
 // flushes the update queue and the pattern histories
 __global__ void tm_reset_kernel(DevCfg c, TmBufs b) {
@@ -343,6 +395,8 @@ int tm_configure_lds(const DevCfg& c) {
          tmk_attr_run_frozen_tm(tm_step_lds_bytes(c, 0, 1, 1)) |
          tmk_attr_run_frozen_spl(b1) | tmk_attr_run_learn_tm(b0);
     r |= hipFuncSetAttribute((const void*)tm_fx_flush_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b1) ==
+                 hipSuccess ? 0 : -1;
+    r |= hipFuncSetAttribute((const void*)tm_lp2_finish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b0) ==
                  hipSuccess ? 0 : -1;
     (void)hipGetLastError();
     return r ? -1 : 0;

@@ -54,6 +54,8 @@ struct __attribute__((aligned(16))) TmSh {
     int32_t fx_na;      // active cells listed by the last frozen collection (U: the cell list)
     uint32_t p1_off;    // LDS offset of the active columns (ascending) phase 1 built infA from
     int32_t p1_n;       // their number, or -1 when infA is not phase 1's
+    int32_t lp2p;       // the previous step's final learnPhase2 is pending (lp2_finish)
+    int32_t lp2s;       // ... and this step's first pool scan has counted its best matches (Tm::lkey)
     float tf[4];
     uint32_t red[3 * TM_NWAVES];
     uint32_t nz_valid;  // the loaded nonzero-column bitmap of colConfidence(t-1) is current (first step)
@@ -76,6 +78,7 @@ struct Tm {
     float* colconf;
     uint32_t* flags;   // ncol bits
     uint32_t* U;       // union region
+    uint32_t* lkey;    // learning: the deferred learnPhase2's best-match keys, u32 [ncol] (lp2_finish)
     uint16_t (*lrnpat)[HTM_MAXACT];  // learn-state pattern ring (learning layouts only)
     // global, this stream
     uint32_t* meta;
@@ -139,7 +142,7 @@ enum { SC_NSCAN = 16, SC_SCANSLOTS, SC_REPLAY, SC_REPLAYCYC, SC_REPLAYSAMPLE, SC
 // ---------------------------------------------------------------------------
 // LDS layout
 struct TmLayout {
-    size_t off_lpat, off_bm, off_conf, off_flags, off_U, total;
+    size_t off_lpat, off_bm, off_conf, off_flags, off_lkey, off_U, total;
     int nbm;
     size_t u_words;
 };
@@ -159,6 +162,8 @@ __host__ __device__ inline TmLayout tm_layout(const DevCfg& c, int learn, int fr
     o = align16(o + (size_t)c.ncol * 4);
     L.off_flags = o;
     o = align16(o + (size_t)c.nw * 4);
+    L.off_lkey = o;  // learning only: the deferred learnPhase2's keys
+    if (learn) o = align16(o + (size_t)c.ncol * 4);
     L.off_U = o;
     // union of phase-local arrays:
     //  finish: colcnt[ncol] u32, nzcol[ncol] u16, nzstart[ncol+1] u32, and the
@@ -453,6 +458,41 @@ __device__ __forceinline__ uint32_t scan_pool(Tm& t, const uint32_t* state, E el
     return nb;
 }
 
+// scan_pool<true> against two cell bitmaps at once: f(slot, meta, live,
+// mask onto `state`, mask onto `state2`) -- one pass over the pool for two
+// counts (an inference phase 2 and the previous step's deferred learn phase 2,
+// collect_scan).  Returns this thread's bytes (the rows counted once).
+template <typename F>
+__device__ __forceinline__ uint32_t scan_pool2(Tm& t, const uint32_t* state, const uint32_t* state2, F f) {
+    const uint32_t hwm = t.sh->hwm;
+    COUNT(t, SC_NSCAN, 1);
+    COUNT(t, SC_SCANSLOTS, hwm);
+    const uint32_t g = threadIdx.x >> 2, sub = threadIdx.x & 3;
+    const uint32_t cwm1 = (uint32_t)t.c.cw - 1u;
+    uint32_t nb = 0, nb2 = 0;
+    for (uint32_t base = 0; base < hwm; base += SC_DEPTH * (TM_NT / 4)) {
+        uint32_t m[SC_DEPTH];
+        uint4 v[SC_DEPTH];
+#pragma unroll
+        for (int d = 0; d < SC_DEPTH; d++) {
+            const uint32_t slot = base + d * (TM_NT / 4) + g;
+            m[d] = slot < hwm ? t.meta[slot] : 0u;
+            v[d] = slot < hwm ? *reinterpret_cast<const uint4*>(t.src + (size_t)slot * HTM_MAXSYN + sub * 8)
+                              : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int d = 0; d < SC_DEPTH; d++) {
+            const uint32_t slot = base + d * (TM_NT / 4) + g;
+            if (slot < hwm && sub == 0) nb += 4;
+            const bool el = meta_live(m[d]);
+            const uint32_t mask = scan_seg_mask(state, cwm1, sub, m[d], el, v[d], nb);
+            const uint32_t mask2 = scan_seg_mask(state2, cwm1, sub, m[d], el, v[d], nb2);
+            f(slot, m[d], el, mask, mask2);
+        }
+    }
+    return nb;
+}
+
 // A scan whose eligible segments are few (learn phase 1: the segments of a
 // handful of flagged columns): the meta words are streamed SCS_META per thread
 // per round trip and the eligible slots listed in LDS (elist[0] the count,
@@ -524,17 +564,42 @@ __device__ __forceinline__ uint32_t scan_pool_sparse(Tm& t, const uint32_t* stat
 
 // collect slots of segments with >= thr synapses onto active cells of
 // `state` by scanning the pool (learning-on form)
+// The first pool scan of a learning step also counts the previous step's
+// deferred learn phase 2 (lp2_finish): every live segment's synapses onto
+// lrnActiveState(t-1), its key (activity, cellInColumn, first slot) kept per
+// column in Tm::lkey -- the pool between the two is the same (the deferred
+// phase writes no segment, and an inference phase 2 writes only dutyCycle
+// records, which it does not read).
 __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
+    const DevCfg& c = t.c;
     const uint32_t sub = threadIdx.x & 3;
-    uint32_t nb = scan_pool<true>(t, state, [](uint32_t) { return true; },
-                            [&](uint32_t slot, uint32_t, bool el, uint32_t mask) {
-                                if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) {
-                                    const uint32_t i = (uint32_t)atomicAdd(&t.sh->qn, 1);
-                                    if (i < (uint32_t)t.c.q_cap) t.q1[i] = slot;
-                                }
-                            });
+    auto qual = [&](uint32_t slot, bool el, uint32_t mask) {
+        if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) {
+            const uint32_t i = (uint32_t)atomicAdd(&t.sh->qn, 1);
+            if (i < (uint32_t)c.q_cap) t.q1[i] = slot;
+        }
+    };
+    uint32_t nb;
+    const bool lp2 = t.lkey != nullptr && t.sh->lp2p && !t.sh->lp2s;  // (LDS flags: uniform)
+    if (lp2) {
+        nb = scan_pool2(t, state, t.lrnA1, [&](uint32_t slot, uint32_t m, bool el, uint32_t mask, uint32_t mask2) {
+            qual(slot, el, mask);
+            const uint32_t n2 = __popc(mask2);
+            if (el && sub == 0 && n2 >= (uint32_t)c.act_thr) {
+                const uint32_t cell = meta_cell(m), col = col_of(c, cell);
+                // scan_best's key order in 32 bits (slots < 2^21, DevCfg::lp2_defer)
+                atomicMax(&t.lkey[col], (n2 << 26) | ((cell - col * c.K) << 21) | (0x1FFFFFu - slot));
+            }
+        });
+    } else {
+        nb = scan_pool<true>(t, state, [](uint32_t) { return true; },
+                             [&](uint32_t slot, uint32_t, bool el, uint32_t mask) { qual(slot, el, mask); });
+    }
     nb = wg_sum(t.sh, nb);
-    if (threadIdx.x == 0) t.sh->bytes += nb;
+    if (threadIdx.x == 0) {
+        t.sh->bytes += nb;
+        if (lp2) t.sh->lp2s = 1;  // (every thread has read the flags: wg_sum's barriers)
+    }
     STAMP(t, SB_SCAN);
 }
 
@@ -1059,28 +1124,46 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
     COUNT(t, SC_P2, 1);
     auto col_at = [&](uint32_t k) -> uint32_t { return in_lds ? (uint32_t)lcol[k] : gcol[k]; };
     auto dc_at = [&](uint32_t k) -> float { return in_lds ? ldc[k] : gdc[k]; };
-    // run heads sum their column in list order, four entries loaded at a time
-    // (the adds stay sequential: NuPIC's float order)
+    // run heads sum their column in list order (the adds stay sequential:
+    // NuPIC's float order), RSG entries per round with the next round's loads
+    // issued before this round's adds -- a bursting step's longest runs
+    // (hundreds of a popular column's segments) were a chain of LDS round
+    // trips, four entries each (tail stamps: 38 K cycles, profiles/r05_ab)
+#ifndef HTM_RSG
+#define HTM_RSG 8
+#endif
+    constexpr uint32_t RSG = HTM_RSG;
     for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
         const uint32_t col = col_at(k);
         if (k > 0 && col_at(k - 1) == col) continue;
         float sum = 0.0f;
-        for (uint32_t j = k;; j += 4) {
-            uint32_t cc[4];
-            float dd[4];
+        uint32_t cc[RSG], cn[RSG];
+        float dd[RSG], dn[RSG];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const bool in = j + u < qn;
-                cc[u] = in ? col_at(j + u) : 0xFFFFFFFFu;
-                dd[u] = in ? dc_at(j + u) : 0.0f;
+        for (uint32_t u = 0; u < RSG; u++) {
+            const bool in = k + u < qn;
+            cc[u] = in ? col_at(k + u) : 0xFFFFFFFFu;
+            dd[u] = in ? dc_at(k + u) : 0.0f;
+        }
+        for (uint32_t j = k;; j += RSG) {
+#pragma unroll
+            for (uint32_t u = 0; u < RSG; u++) {
+                const bool in = j + RSG + u < qn;
+                cn[u] = in ? col_at(j + RSG + u) : 0xFFFFFFFFu;
+                dn[u] = in ? dc_at(j + RSG + u) : 0.0f;
             }
             bool stop = false;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (uint32_t u = 0; u < RSG; u++) {
                 if (!stop && cc[u] == col) sum += dd[u];
                 else stop = true;
             }
             if (stop) break;
+#pragma unroll
+            for (uint32_t u = 0; u < RSG; u++) {
+                cc[u] = cn[u];
+                dd[u] = dn[u];
+            }
         }
         t.colconf[col] = sum;
     }
@@ -2543,39 +2626,25 @@ __device__ __forceinline__ bool learn_phase1(Tm& t, const uint16_t* cols, int nA
     return inSeq;
 }
 
-// _learnPhase2(readOnly).  A read-only pass of a learn backtrack (`next`: the
-// columns of the pattern after it) computes lrnPredictedState only for those
-// columns: its one reader is the next pattern's read-only _learnPhase1, which
-// looks at the next pattern's columns alone (learn_backtrack_from); every
-// pass that writes recomputes lrnP in full before anything else reads it.
-// The best-match search then reads the rows of those columns' segments only
-// (scan_best's flagged form) instead of the whole pool.
-__device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* next = nullptr, int nnext = 0) {
+// The rest of _learnPhase2 once its best-match keys are in U (u64 [ncol]):
+// lrnPredictedState into `out` (cleared by the caller) and, unless read-only,
+// the queued segment updates of the columns with a key -- active synapses and
+// new-synapse candidates against `state` (lrnActiveState of the step the phase
+// belongs to), dated `date`.  The step's own phase: (lrnA, lrnP, lrn_iter); the
+// previous step's deferred one (lp2_finish): (lrnA1, lrnP1, lrn_iter - 1).
+__device__ __forceinline__ void learn_phase2_post(Tm& t, const uint32_t* state, uint32_t* out, uint32_t date,
+                                                  bool ro) {
     const DevCfg& c = t.c;
     TmSh* sh = t.sh;
     const int K = c.K;
-    if (threadIdx.x == 0) sh->st[2]++;
-    wg_clear(t.lrnP, c.cw);
-    wg_clear(t.U, 2 * c.ncol);
-    const bool part = ro && next != nullptr;
-    if (part) {
-        wg_clear(t.flags, c.nw);
-        __syncthreads();
-        for (int a = threadIdx.x; a < nnext; a += TM_NT) atomicOr(&t.flags[next[a] >> 5], 1u << (next[a] & 31));
-    }
-    __syncthreads();
-    STAMP(t, SB_LEARN);
-    scan_best(t, t.lrnA, c.act_thr, part ? t.flags : nullptr);
-    __syncthreads();
-    STAMP(t, SB_LSCAN);
     const unsigned long long* keys = reinterpret_cast<const unsigned long long*>(t.U);
     for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
         unsigned long long key = keys[col];
-        if (key) bm_or_field(t.lrnP, (uint32_t)col * K + key_cic(key), 1, 1u);
+        if (key) bm_or_field(out, (uint32_t)col * K + key_cic(key), 1, 1u);
     }
     __syncthreads();
     if (ro) return;
-    build_cand(t, t.lrnA);
+    build_cand(t, state);
     STAMP(t, SB_LEARN);
 #ifdef HTM_LEARN_SERIAL
     if (wave_id() == 0) {
@@ -2589,7 +2658,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* nex
                 uint32_t slot = key_slot(key), act = key_act(key);
                 COUNT(t, SC_LP2COLS, 1);
                 STAMP(t, SB_LW);
-                WUpd u = w_build_update(t, slot, t.lrnA, act < (uint32_t)c.new_syn);
+                WUpd u = w_build_update(t, slot, state, act < (uint32_t)c.new_syn);
                 STAMP(t, SB_LWB);
                 if (u.mask == 0u && u.n_new == 0u) continue;
                 int idx = sh->n_upd;
@@ -2605,7 +2674,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* nex
                     e.cell = (uint8_t)key_cic(key);
                     e.n_new = (uint8_t)u.n_new;
                     e.active_mask = u.mask;
-                    e.date = sh->lrn_iter;
+                    e.date = date;
                     sh->n_upd = idx + 1;
                     // queued entry written now and read back at the next step
                     atomicAdd(&sh->bytes, (unsigned long long)(2 * (16 + 2 * u.n_new)));
@@ -2637,7 +2706,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* nex
             const uint32_t col = kc[b0 + j];
             const unsigned long long key = keys[col];
             const uint32_t slot = key_slot(key);
-            w_rec_build(t, &recs[j], LR_QUEUE, col, key_cic(key), slot, t.meta[slot], t.lrnA,
+            w_rec_build(t, &recs[j], LR_QUEUE, col, key_cic(key), slot, t.meta[slot], state,
                         key_act(key) < (uint32_t)c.new_syn);
             COUNT(t, SC_LP2COLS, 1);
         }
@@ -2660,7 +2729,7 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* nex
                 e.cell = r.cic;
                 e.n_new = (uint8_t)nn;
                 e.active_mask = r.mask;
-                e.date = sh->lrn_iter;
+                e.date = date;
                 // queued entry written now and read back at the next step
                 atomicAdd(&sh->bytes, (unsigned long long)(2 * (16 + 2 * nn)));
             }
@@ -2671,6 +2740,74 @@ __device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* nex
 #endif
     __syncthreads();
     STAMP(t, SB_LW);
+}
+
+// _learnPhase2(readOnly).  A read-only pass of a learn backtrack (`next`: the
+// columns of the pattern after it) computes lrnPredictedState only for those
+// columns: its one reader is the next pattern's read-only _learnPhase1, which
+// looks at the next pattern's columns alone (learn_backtrack_from); every
+// pass that writes recomputes lrnP in full before anything else reads it.
+// The best-match search then reads the rows of those columns' segments only
+// (scan_best's flagged form) instead of the whole pool.
+__device__ __forceinline__ void learn_phase2(Tm& t, bool ro, const uint16_t* next = nullptr, int nnext = 0) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    if (threadIdx.x == 0) sh->st[2]++;
+    wg_clear(t.lrnP, c.cw);
+    wg_clear(t.U, 2 * c.ncol);
+    const bool part = ro && next != nullptr;
+    if (part) {
+        wg_clear(t.flags, c.nw);
+        __syncthreads();
+        for (int a = threadIdx.x; a < nnext; a += TM_NT) atomicOr(&t.flags[next[a] >> 5], 1u << (next[a] & 31));
+    }
+    __syncthreads();
+    STAMP(t, SB_LEARN);
+    scan_best(t, t.lrnA, c.act_thr, part ? t.flags : nullptr);
+    __syncthreads();
+    STAMP(t, SB_LSCAN);
+    learn_phase2_post(t, t.lrnA, t.lrnP, sh->lrn_iter, ro);
+}
+
+// The final _learnPhase2 of a learning step is deferred (DevCfg::lp2_defer):
+// the step ends with it pending (TmSh::lp2p, htm_tm_header::lp2_pending) and
+// the next step completes it -- its best-match count rides on that step's
+// first pool scan (collect_scan, keys in Tm::lkey), its lrnPredictedState
+// goes straight into lrnP1, and its queued updates and nupic::Random draws
+// happen after that step's inference and before its learning.  Nothing in
+// between reads or writes what the phase reads or writes: inference touches
+// no learn state, queue or generator, and only dutyCycle records of the
+// segments; a step's learning starts with processSegmentUpdates, after this.
+// Saves one full pool scan per learning step.  `date`: the deferred phase's
+// lrn_iter.  A pending phase whose keys were not counted (no pool scan ran)
+// scans here.  The engine completes a pending phase (tm_lp2_finish_kernel)
+// before anything reads the state or steps without learning.
+__device__ __forceinline__ void lp2_finish(Tm& t, uint32_t date) {
+    const DevCfg& c = t.c;
+    TmSh* sh = t.sh;
+    if (threadIdx.x == 0) sh->st[2]++;
+    wg_clear(t.lrnP1, c.cw);
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(t.U);
+    if (!sh->lp2s) {
+        wg_clear(t.U, 2 * c.ncol);
+        __syncthreads();
+        scan_best(t, t.lrnA1, c.act_thr, nullptr);
+    } else {
+        for (int col = threadIdx.x; col < c.ncol; col += TM_NT) {
+            const uint32_t k = t.lkey[col];
+            keys[col] = k ? ((unsigned long long)(k >> 26) << 40) | ((unsigned long long)((k >> 21) & 31u) << 32) |
+                                (unsigned long long)(0xFFFFFFFFu - (0x1FFFFFu - (k & 0x1FFFFFu)))
+                          : 0ull;
+        }
+    }
+    __syncthreads();
+    STAMP(t, SB_LSCAN);
+    learn_phase2_post(t, t.lrnA1, t.lrnP1, date, false);
+    if (threadIdx.x == 0) {
+        sh->lp2p = 0;
+        sh->lp2s = 0;
+    }
+    __syncthreads();
 }
 
 // start cells (cell 0) of the given columns into lrnA
@@ -2811,7 +2948,16 @@ __device__ __forceinline__ void update_learning(Tm& t) {
         }
         __syncthreads();
     }
-    learn_phase2(t, false);
+    if (c.lp2_defer) {
+        // the final learn phase 2: completed by the next step (lp2_finish)
+        if (threadIdx.x == 0) {
+            sh->lp2p = 1;
+            sh->lp2s = 0;
+        }
+        __syncthreads();
+    } else {
+        learn_phase2(t, false);
+    }
 }
 
 // stable compaction of live segments (slot order preserved) so that a
@@ -2902,6 +3048,7 @@ __device__ __forceinline__ void tm_bind(Tm& t, const DevCfg& c, const TmBufs& b,
     t.colconf = reinterpret_cast<float*>(lds + L.off_conf);
     t.flags = reinterpret_cast<uint32_t*>(lds + L.off_flags);
     t.U = reinterpret_cast<uint32_t*>(lds + L.off_U);
+    t.lkey = LEARN ? reinterpret_cast<uint32_t*>(lds + L.off_lkey) : nullptr;
     t.lrnpat = LEARN ? reinterpret_cast<uint16_t(*)[HTM_MAXACT]>(lds + L.off_lpat) : nullptr;
     const size_t sc = (size_t)c.seg_cap;
     // model buffers: the stream's own, or the fleet's shared instance 0
@@ -3127,6 +3274,8 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
             sh->st[1] = hdr->stat_inf_backtrack;
             sh->st[2] = hdr->stat_lrn_phase2;
             sh->st[3] = hdr->stat_lrn_backtrack;
+            sh->lp2p = LEARN ? (int32_t)hdr->lp2_pending : 0;
+            sh->lp2s = 0;
             uint32_t na = sp.nact[s];
             sh->nA = (int32_t)(na < HTM_MAXACT ? na : HTM_MAXACT);
             sh->nz_valid = gnzr[c.nw];
@@ -3202,6 +3351,10 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         }
     }
     __syncthreads();
+    if (LEARN && sh->lp2p) {  // the deferred learn phase 2's keys (collect_scan)
+        wg_clear(t.lkey, c.ncol);
+        __syncthreads();
+    }
     STAMP(t, SB_LOAD);
     if (LEARN && sh->hwm + (uint32_t)c.seg_reserve > (uint32_t)c.seg_cap) {
         compact_pool(t);
@@ -3210,6 +3363,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
     // ---- BacktrackingTM.compute(input, learn, infer=True)
     update_inference<FROZEN>(t);
     STAMP(t, SB_BT);
+    if (LEARN && sh->lp2p) lp2_finish(t, sh->lrn_iter - 1u);  // (the previous step's lrn_iter)
     if (LEARN) update_learning(t);
     STAMP(t, SB_LEARN);
     // ---- write back (last step of the run only)
@@ -3308,6 +3462,7 @@ __device__ __forceinline__ void tm_step_body(const DevCfg& c, const TmBufs& b, c
         hdr->stat_inf_backtrack = sh->st[1];
         hdr->stat_lrn_phase2 = sh->st[2];
         hdr->stat_lrn_backtrack = sh->st[3];
+        if (LEARN) hdr->lp2_pending = (uint32_t)sh->lp2p;
     }
 #ifdef HTM_STAMPS
     __syncthreads();

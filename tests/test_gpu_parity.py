@@ -287,3 +287,39 @@ def test_run_units_equal_lockstep_steps(rt, unit):
         sa, sb = a.tm_states(s), b.tm_states(s)
         for k in sa:
             assert np.array_equal(sa[k], sb[k])
+
+
+def test_deferred_learn_phase2_completed_anywhere(rt, oracle_mod):
+    """A learning step leaves its final learn phase 2 pending (tm_core.h
+    lp2_finish: the next step's first pool scan counts it).  Completing it
+    early -- a state export (tm_lp2_finish_kernel) in the middle of lockstep
+    learning, a mid-run save/load, an htm_run chunk boundary -- changes no
+    result: scores at every step and the final SP/TM state equal an engine
+    that never stops, and both equal the oracle."""
+    n = 3
+    rng = np.random.default_rng(5)
+    vals = np.clip(np.tile(rng.integers(0, 101, size=(12, 1)), (8, n)) + rng.integers(-3, 4, size=(96, n)), 0, 100)
+    vals = vals.astype(np.float64)
+    v = torch.tensor(vals, device="cuda")
+    a = rt.HTMEngine(n, seed_stride=1, seg_capacity=1 << 12)
+    b = rt.HTMEngine(n, seed_stride=1, seg_capacity=1 << 12)
+    orcs = [oracle_mod.OracleModel(sp_seed=2045 + s, tm_seed=2045 + s) for s in range(n)]
+    for e in (a, b):
+        e.set_learning(True, True)
+    got_a, got_b = [], []
+    for k in range(96):
+        got_a.append(a.step(v[k]).cpu().numpy())
+        if k % 7 == 3:
+            a.export_state("tm_header")  # completes the pending phase mid-run
+        if k == 50:
+            got_b.append(b.run(v[50:70]).cpu().numpy())
+        elif not 50 < k < 70:
+            got_b.append(b.step(v[k]).cpu().numpy()[None])
+    ga, gb = np.stack(got_a), np.concatenate(got_b)
+    assert np.array_equal(ga, gb)
+    for s in range(n):
+        want = np.array([orcs[s].step([vals[k, s]], True, True) for k in range(96)], np.float32)
+        assert np.array_equal(ga[:, s], want), f"stream {s}"
+        tm_equal(a, s, orcs[s])
+        tm_equal(b, s, orcs[s])
+        assert a.tm_header(s).lp2_pending == 0
