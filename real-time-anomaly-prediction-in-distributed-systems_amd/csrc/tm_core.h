@@ -1125,45 +1125,75 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
     auto col_at = [&](uint32_t k) -> uint32_t { return in_lds ? (uint32_t)lcol[k] : gcol[k]; };
     auto dc_at = [&](uint32_t k) -> float { return in_lds ? ldc[k] : gdc[k]; };
     // run heads sum their column in list order (the adds stay sequential:
-    // NuPIC's float order), RSG entries per round with the next round's loads
-    // issued before this round's adds -- a bursting step's longest runs
-    // (hundreds of a popular column's segments) were a chain of LDS round
-    // trips, four entries each (tail stamps: 38 K cycles, profiles/r05_ab)
-#ifndef HTM_RSG
-#define HTM_RSG 8
+    // NuPIC's float order).  In LDS a run is read in aligned groups of eight
+    // entries -- one 16-byte read of the columns, two of the dutyCycles --
+    // with the next group's reads issued before this group's adds: a bursting
+    // step's longest runs (hundreds of a popular column's segments) were a
+    // chain of four-entry rounds of scalar reads (tail stamps: sums 38 K
+    // cycles, profiles/r05_ab); wider scalar prefetches measured slower (LDS
+    // issue, profiles/r06_ab/run_sums)
+#ifndef HTM_SUMS_OLD
+    if (in_lds) {
+        const uint4* lc4 = reinterpret_cast<const uint4*>(lcol);  // (U and ql/2 words: 16-byte aligned)
+        const float4* ld4 = reinterpret_cast<const float4*>(ldc);
+        for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
+            const uint32_t col = lcol[k];
+            if (k > 0 && lcol[k - 1] == col) continue;
+            float sum = 0.0f;
+            uint32_t a = k & ~7u;  // the group holding k
+            uint4 cg = lc4[a >> 3];
+            float4 d0 = ld4[a >> 2], d1 = ld4[(a >> 2) + 1];
+            uint32_t i = k - a;  // the first entry of the run in the group
+            for (;;) {
+                const bool more = a + 8u < qn;
+                uint4 cgn = make_uint4(0u, 0u, 0u, 0u);
+                float4 d0n = make_float4(0.f, 0.f, 0.f, 0.f), d1n = d0n;
+                if (more) {
+                    cgn = lc4[(a >> 3) + 1];
+                    d0n = ld4[(a >> 2) + 2];
+                    d1n = ld4[(a >> 2) + 3];
+                }
+                const uint32_t cw[4] = {cg.x, cg.y, cg.z, cg.w};
+                const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+                bool stop = false;
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    if (u < i) continue;
+                    const uint32_t cu = (cw[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu;
+                    if (!stop && a + u < qn && cu == col) sum += dv[u];
+                    else stop = true;
+                }
+                if (stop || !more) break;
+                a += 8u;
+                i = 0u;
+                cg = cgn;
+                d0 = d0n;
+                d1 = d1n;
+            }
+            t.colconf[col] = sum;
+        }
+    } else
 #endif
-    constexpr uint32_t RSG = HTM_RSG;
     for (uint32_t k = threadIdx.x; k < qn; k += TM_NT) {
         const uint32_t col = col_at(k);
         if (k > 0 && col_at(k - 1) == col) continue;
         float sum = 0.0f;
-        uint32_t cc[RSG], cn[RSG];
-        float dd[RSG], dn[RSG];
+        for (uint32_t j = k;; j += 4) {
+            uint32_t cc[4];
+            float dd[4];
 #pragma unroll
-        for (uint32_t u = 0; u < RSG; u++) {
-            const bool in = k + u < qn;
-            cc[u] = in ? col_at(k + u) : 0xFFFFFFFFu;
-            dd[u] = in ? dc_at(k + u) : 0.0f;
-        }
-        for (uint32_t j = k;; j += RSG) {
-#pragma unroll
-            for (uint32_t u = 0; u < RSG; u++) {
-                const bool in = j + RSG + u < qn;
-                cn[u] = in ? col_at(j + RSG + u) : 0xFFFFFFFFu;
-                dn[u] = in ? dc_at(j + RSG + u) : 0.0f;
+            for (int u = 0; u < 4; u++) {
+                const bool in = j + u < qn;
+                cc[u] = in ? col_at(j + u) : 0xFFFFFFFFu;
+                dd[u] = in ? dc_at(j + u) : 0.0f;
             }
             bool stop = false;
 #pragma unroll
-            for (uint32_t u = 0; u < RSG; u++) {
+            for (int u = 0; u < 4; u++) {
                 if (!stop && cc[u] == col) sum += dd[u];
                 else stop = true;
             }
             if (stop) break;
-#pragma unroll
-            for (uint32_t u = 0; u < RSG; u++) {
-                cc[u] = cn[u];
-                dd[u] = dn[u];
-            }
         }
         t.colconf[col] = sum;
     }
@@ -1203,6 +1233,16 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
             // (16 heads per round: four 16-byte reads issued together, then the
             // adds -- a chunk holds 64 slots, so reads past its count stay in it)
             float tot = 0.0f;
+            auto fold16 = [&](const float4 (&x)[4], uint32_t j, uint32_t nn) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t k = j + 4u * u;
+                    tot += k < nn ? x[u].x : 0.0f;
+                    tot += k + 1 < nn ? x[u].y : 0.0f;
+                    tot += k + 2 < nn ? x[u].z : 0.0f;
+                    tot += k + 3 < nn ? x[u].w : 0.0f;
+                }
+            };
             uint32_t nn1 = nch ? cnt[0] : 0u;
             for (uint32_t ch = 0; ch < nch; ch++) {
                 const uint32_t nn = nn1;
@@ -1212,14 +1252,7 @@ __device__ __forceinline__ uint32_t phase2_finish_ranked(Tm& t) {
                     float4 x[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++) x[u] = p[(j >> 2) + u];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t k = j + 4u * u;
-                        tot += k < nn ? x[u].x : 0.0f;
-                        tot += k + 1 < nn ? x[u].y : 0.0f;
-                        tot += k + 2 < nn ? x[u].z : 0.0f;
-                        tot += k + 3 < nn ? x[u].w : 0.0f;
-                    }
+                    fold16(x, j, nn);
                 }
             }
             if (lane_id() == 0) sh->tf[0] = tot;
