@@ -278,13 +278,22 @@ int launch_sp_perm_import(const DevCfg& c, const SpBufs& b, const float* src, si
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The boosted inhibition's keys ((nw + 1) * 32 words) as dynamic LDS of the
+// learning SP kernels, only when boostStrength != 0 (model.yaml): a static
+// array sized for 4,096 columns (16.5 KiB) held every Model-1 learning SP
+// workgroup to three per CU (41.5 KiB).
+static size_t sp_bkey_lds(const DevCfg& c, int learn) {
+    return learn && c.sp_boost != 0.0f ? (size_t)(c.nw + 1) * 32 * 4 : 0;
+}
+
 // ---------------------------------------------------------------------------
 template <bool LEARN>
 __global__ __launch_bounds__(256) void sp_step_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps,
                                                       const uint16_t* enc) {
     __shared__ SpShared sh;
-    __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
-    sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps, LEARN ? bkey : nullptr, enc);
+    extern __shared__ __attribute__((aligned(16))) uint32_t sp_dyn[];  // boosted inhibition (sp_bkey_lds)
+    sp_step_body<LEARN>(c, b, values, blockIdx.x, sh, write_overlaps, LEARN && c.sp_boost != 0.0f ? sp_dyn : nullptr,
+                        enc);
 }
 
 // The SP of a split lockstep step, the fused kernel's four-wave SP (its
@@ -299,10 +308,16 @@ template <bool LEARN, bool PAGED>
 __global__ __launch_bounds__(256) void sp_step_ord_kernel(DevCfg c, SpBufs b, const double* values, int write_overlaps,
                                                           const uint16_t* enc, const uint32_t* tm_bm, uint16_t* est) {
     __shared__ SpShared sh;
-    __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
+    extern __shared__ __attribute__((aligned(16))) uint32_t sp_dyn[];  // boosted inhibition (sp_bkey_lds)
     __shared__ uint32_t planes[SP_PLANE_WORDS];
     const int s = blockIdx.x;
-    sp_step_body<LEARN, PAGED, true>(c, b, values, s, sh, write_overlaps, LEARN ? bkey : nullptr, enc, planes);
+#ifdef HTM_SP_BKEY_STATIC  // (A/B builds: the round-5 static LDS footprint, 41.5 KiB)
+    __shared__ uint32_t pad_[LEARN ? (HTM_MAXNW + 1) * 32 : 1];
+    if (threadIdx.x == 0 && values == nullptr && enc == nullptr) pad_[s & 7] = 0u;
+    if (threadIdx.x == 0 && values == nullptr && enc == nullptr) planes[0] = pad_[(s + 1) & 7];
+#endif
+    sp_step_body<LEARN, PAGED, true>(c, b, values, s, sh, write_overlaps,
+                                     LEARN && c.sp_boost != 0.0f ? sp_dyn : nullptr, enc, planes);
     if (!est) return;
     __syncthreads();
     if (wave_id() == 0) {
@@ -323,10 +338,10 @@ int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, i
                        const uint32_t* tm_bm, uint16_t* est, hipStream_t st) {
     const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? b.enc_in : nullptr;  // (one step: row 0)
     if (learn && c.sp_paged)
-        hipLaunchKernelGGL((sp_step_ord_kernel<true, true>), dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps,
+        hipLaunchKernelGGL((sp_step_ord_kernel<true, true>), dim3(n), dim3(256), sp_bkey_lds(c, 1), st, c, b, values, keep_overlaps,
                            enc, tm_bm, est);
     else if (learn)
-        hipLaunchKernelGGL((sp_step_ord_kernel<true, false>), dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps,
+        hipLaunchKernelGGL((sp_step_ord_kernel<true, false>), dim3(n), dim3(256), sp_bkey_lds(c, 1), st, c, b, values, keep_overlaps,
                            enc, tm_bm, est);
     else
         hipLaunchKernelGGL((sp_step_ord_kernel<false, false>), dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps,
@@ -339,14 +354,14 @@ int launch_sp_step_ord(const DevCfg& c, const SpBufs& b, const double* values, i
 template <bool LEARN>
 __global__ __launch_bounds__(256) void sp_step_sdr_kernel(DevCfg c, SpBufs b, const uint32_t* sdr, int write_overlaps) {
     __shared__ SpSharedSdr sh;
-    __shared__ uint32_t bkey[LEARN ? (HTM_MAXNW + 1) * 32 : 1];  // boosted inhibition
-    sp_step_body<LEARN>(c, b, sdr, blockIdx.x, sh, write_overlaps, LEARN ? bkey : nullptr);
+    extern __shared__ __attribute__((aligned(16))) uint32_t sp_dyn[];  // boosted inhibition (sp_bkey_lds)
+    sp_step_body<LEARN>(c, b, sdr, blockIdx.x, sh, write_overlaps, LEARN && c.sp_boost != 0.0f ? sp_dyn : nullptr);
 }
 
 int launch_sp_step_sdr(const DevCfg& c, const SpBufs& b, const uint32_t* sdr, int learn, int n, int keep_overlaps,
                        hipStream_t st) {
     if (learn)
-        hipLaunchKernelGGL(sp_step_sdr_kernel<true>, dim3(n), dim3(256), 0, st, c, b, sdr, keep_overlaps);
+        hipLaunchKernelGGL(sp_step_sdr_kernel<true>, dim3(n), dim3(256), sp_bkey_lds(c, 1), st, c, b, sdr, keep_overlaps);
     else
         hipLaunchKernelGGL(sp_step_sdr_kernel<false>, dim3(n), dim3(256), 0, st, c, b, sdr, keep_overlaps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -356,7 +371,7 @@ int launch_sp_step(const DevCfg& c, const SpBufs& b, const double* values, int l
                    hipStream_t st) {
     const uint16_t* enc = c.enc_type == HTM_ENC_RDSE ? b.enc_in : nullptr;  // (one step: row 0)
     if (learn)
-        hipLaunchKernelGGL(sp_step_kernel<true>, dim3(n), dim3(256), 0, st, c, b, values, keep_overlaps, enc);
+        hipLaunchKernelGGL(sp_step_kernel<true>, dim3(n), dim3(256), sp_bkey_lds(c, 1), st, c, b, values, keep_overlaps, enc);
     else
         hipLaunchKernelGGL(sp_step_kernel<false>, dim3(n), dim3(64), 0, st, c, b, values, keep_overlaps, enc);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -56,3 +56,26 @@ def test_standin_scores_are_a_function_of_the_global_stream():
     e.step(torch.tensor([3.0, 4.0, 5.0, 6.0], dtype=torch.float64), out)
     want = np.array([standin_score(10 + i, 3 + i) for i in range(4)], np.float32)
     assert np.array_equal(out.numpy(), want)
+
+
+def test_config5_inputs_follow_the_aggregate_schema():
+    """bench.py's config-5 workload (no GPU): the four aggregate fields in the
+    MultiEncoder's sorted order (cpu, max, mean, mem), each stream's records
+    the reference's TestingData aggregates shifted by 97 records, cpu/mem
+    jittered and clipped to [0, 100], response times scaled per stream; a
+    stream's shard of the inputs equals the same streams of the whole; the
+    training rows skip records with a null field (ModelTraining.py:29-32)."""
+    import bench
+    d = np.load(os.path.join(ROOT, "tests", "golden", "model1_traces.npz"))
+    assert [f[0] for f in bench.FIELDS5] == sorted(f[0] for f in bench.FIELDS5)
+    rec, mean, viol = bench.config5_inputs(d, 8, 0, 8, 12)
+    assert rec.shape == (12, 8, 4) and mean.shape == (12, 8) and viol.shape == (12, 8)
+    assert np.all((rec[..., 0] >= 0) & (rec[..., 0] <= 100) & (rec[..., 3] >= 0) & (rec[..., 3] <= 100))
+    idx = (np.arange(12)[:, None] + 97 * np.arange(8)[None, :]) % len(d["test_cpu"])
+    assert np.all(np.abs(rec[..., 0] - d["test_cpu"][idx]) <= 2 + 1e-9)
+    np.testing.assert_array_equal(rec[..., 2], mean)
+    np.testing.assert_array_equal(viol, d["test_violations"][idx])
+    part, _, _ = bench.config5_inputs(d, 8, 3, 6, 12)
+    np.testing.assert_array_equal(part, rec[:, 3:6])
+    tr = bench.config5_train_values(d)
+    assert tr.shape[1] == 4 and len(tr) <= 2184 and not np.isnan(tr).any()
