@@ -59,40 +59,44 @@ def run():
 
 
 def analyse(path, js):
+    """Per region (from a marker kernel to the last flush-done kernel before
+    the next marker): the GPU span, when the first step's SP kernel starts
+    after the marker, the TM launches, the flushes beside the steps and the
+    final flush after the last TM launch."""
     rows = list(csv.DictReader(open(path)))
-    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
+    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]) for r in rows)
     info = json.load(open(js)) if js else None
-    marks = [i for i, k in enumerate(ks) if "elementwise" in k[2] or "vectorized" in k[2]]
+    marks = [i for i, k in enumerate(ks) if "elementwise" in k[2]]
     res = []
     for j, m in enumerate(marks):
-        end = marks[j + 1] if j + 1 < len(marks) else len(ks)
-        seg = ks[m:end]
-        # the region's kernels: up to the last flush-done kernel before the next marker
-        last = max(i for i, k in enumerate(seg) if "flush_done" in k[2]) if any("flush_done" in k[2] for k in seg) else len(seg) - 1
-        seg = seg[:last + 1]
+        seg = ks[m:marks[j + 1] if j + 1 < len(marks) else len(ks)]
+        done = [i for i, k in enumerate(seg) if "flush_done" in k[2]]
+        if not done:
+            continue
+        seg = seg[:done[-1] + 1]
         t0 = seg[0][0]
-        tm = [k for k in seg if "frozen_tm" in k[2] or "htm_run_frozen_kernel" in k[2]]
-        busy = 0
-        cur_s, cur_e = None, None
-        for s, e, _ in seg:  # union of kernel intervals (the flush stream overlaps the steps)
-            if cur_e is None or s > cur_e:
-                if cur_e is not None:
-                    busy += cur_e - cur_s
-                cur_s, cur_e = s, e
-            else:
-                cur_e = max(cur_e, e)
-        busy += cur_e - cur_s
-        first_step = next(k for k in seg if "sp_step" in k[2])
-        fin = [k for k in seg if "fx_" in k[2] and k[0] >= tm[-1][1]]
-        res.append({"gpu_span_us": round((seg[-1][1] - t0) / 1e3, 1), "gpu_busy_us": round(busy / 1e3, 1),
-                    "marker_to_first_step_us": round((first_step[0] - seg[0][1]) / 1e3, 1),
-                    "tm_launch_us_mean": round(float(np.mean([(e - s) / 1e3 for s, e, _ in tm])), 1),
-                    "last_tm_end_to_region_end_us": round((seg[-1][1] - tm[-1][1]) / 1e3, 1),
-                    "after_last_step": [(k[2].split("(")[0][:40], round((k[0] - tm[-1][1]) / 1e3, 1),
-                                         round((k[1] - k[0]) / 1e3, 1)) for k in fin]})
+        tm = [k for k in seg if "frozen_tm" in k[2] or k[2] == "htm_run_frozen_kernel"]
+        sp = [k for k in seg if "sp_step" in k[2]]
+        if not tm or not sp:
+            continue
+        fl = [k for k in seg if k[2] == "tm_fx_flush_kernel"]
+        fin = [k for k in seg if k[2].startswith("tm_fx_") and k[0] >= tm[-1][1]]
+        beside = [k for k in fl if k[0] < tm[-1][1]]
+        tmd = [(e - s) / 1e3 for s, e, _ in tm]
+        over = [(e - s) / 1e3 for s, e, _ in tm if any(f[0] < e and f[1] > s for f in beside)]
+        res.append({"gpu_span_us": round((seg[-1][1] - t0) / 1e3, 1),
+                    "marker_to_first_sp_us": round((sp[0][0] - seg[0][1]) / 1e3, 1),
+                    "tm_launches": len(tm), "tm_us_median": round(float(np.median(tmd)), 1),
+                    "tm_us_beside_a_flush": [round(x, 1) for x in over],
+                    "flushes_beside": [round((e - s) / 1e3, 1) for s, e, _ in beside],
+                    "final_flush_us": round((seg[-1][1] - tm[-1][1]) / 1e3, 1),
+                    "final_flush_kernels": [(k[2], round((k[1] - k[0]) / 1e3, 1)) for k in fin]})
     out = {"regions": res}
     if info:
         out["host_region_ms"] = info["region_ms"]
+        n = min(len(res), len(info["region_ms"]))
+        out["host_minus_gpu_us"] = [round(h * 1e3 - r["gpu_span_us"], 1)
+                                    for h, r in zip(info["region_ms"][-n:], res[-n:])]
     print(json.dumps(out, indent=1))
 
 
