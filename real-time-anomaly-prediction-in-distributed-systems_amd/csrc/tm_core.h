@@ -573,10 +573,15 @@ __device__ __forceinline__ uint32_t scan_pool_sparse(Tm& t, const uint32_t* stat
 __device__ __forceinline__ void collect_scan(Tm& t, const uint32_t* state, int thr) {
     const DevCfg& c = t.c;
     const uint32_t sub = threadIdx.x & 3;
+    // a qualifying segment's slot to q1 and its active-synapse mask to q2
+    // (pass 1 reads the mask instead of the segment's row again)
     auto qual = [&](uint32_t slot, bool el, uint32_t mask) {
         if (el && sub == 0 && __popc(mask) >= (uint32_t)thr) {
             const uint32_t i = (uint32_t)atomicAdd(&t.sh->qn, 1);
-            if (i < (uint32_t)c.q_cap) t.q1[i] = slot;
+            if (i < (uint32_t)c.q_cap) {
+                t.q1[i] = slot;
+                t.q2[i] = mask;
+            }
         }
     };
     uint32_t nb;
@@ -634,13 +639,17 @@ __device__ __forceinline__ void fx_owner_map(const uint32_t* pstart, uint32_t na
 // round trip covers FX_OWN blocks whatever the list lengths; the next pass's
 // map is built while those loads are in flight (a barrier once every thread
 // has read the map for its addresses -- LDS reads only: the loads stay in
-// flight), not before the next loads.
+// flight), not before the next loads.  The first pass's map is the
+// caller's (collect_frozen writes it with the list starts, before its
+// barrier; -DHTM_OWNER_SEP builds it here, round 5).
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
                                           uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy,
                                           TmSh* shp = nullptr) {
     if (B == 0) return;
+#ifdef HTM_OWNER_SEP
     fx_owner_map(pstart, na, 0u, B < FX_OWN ? B : FX_OWN, owner);
     __syncthreads();
+#endif
     STAMP_SH(shp, SB_OWNER);
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
@@ -654,8 +663,10 @@ __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo,
                 v[j] = ent[plo[k] + (x - pstart[k])];
             }
         }
-        __syncthreads();  // (every thread's map reads done)
-        if (hi < B) fx_owner_map(pstart, na, hi, B - hi < FX_OWN ? B : hi + FX_OWN, owner);
+        if (hi < B) {
+            __syncthreads();  // (every thread's map reads done)
+            fx_owner_map(pstart, na, hi, B - hi < FX_OWN ? B : hi + FX_OWN, owner);
+        }
         STAMP_SH(shp, SB_OWNER);
 #pragma unroll
         for (int j = 0; j < FX_DEPTH; j++) {
@@ -840,8 +851,11 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
     const int w_first = (pid_ok && t.np > 0 && mode != FX_WIN && mode != FX_WIN_REUSE) ? -1 : win >= 0 ? win : 0;
     const int w_end = mode == FX_PID ? 0 : win >= 0 ? (win < (int)nw ? win + 1 : win) : (int)nw;
     if (w_first < w_end) load_offsets(w_first);
-    for (int w = w_first; w < w_end; w++) {
-        // list of (active cell k, pass w): block range [fxoff[idx], fxoff[idx + 1])
+    // this thread's lists of pass w: plo = the first block, pstart = the block
+    // count (the exclusive prefix replaces it once the workgroup total is
+    // known); returns their block total.  olo/ohi hold pass w's first FX_PF
+    // offsets (loaded a pass ahead); pass w + 1's are requested here.
+    auto store_lists = [&](int w) {
         uint32_t lsum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < FX_PF; j++) {
@@ -862,29 +876,43 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
             lsum += hi - lo;
         }
         if (w + 1 < w_end) load_offsets(w + 1);
-        uint32_t B;
-        uint32_t pos = wg_excl_scan1(sh, lsum, &B);
+        return lsum;
+    };
+    // the lists' starts from this thread's exclusive prefix pos, and
+    // fx_stream's first block -> list map from the starts in hand
+    auto place_lists = [&](uint32_t pos, uint32_t B) {
         for (uint32_t j = 0; j < per; j++) {
             const uint32_t k = k0 + j;
             if (k >= na) break;
             const uint32_t n = pstart[k];
             pstart[k] = pos;
+#ifndef HTM_OWNER_SEP
+            const uint32_t e = pos + n < FX_OWN ? pos + n : FX_OWN;
+            for (uint32_t x = pos; x < e; x++) owner[x] = (uint16_t)k;
+#endif
             pos += n;
         }
         if (threadIdx.x == 0) pstart[na] = B;
-        nblk += B;
+    };
+    for (int w = w_first; w < w_end; w++) {
         // counters cover the pids (pass -1) or this window's ranks
         const uint32_t span = w < 0 ? t.np : (nr - (uint32_t)w * W < W ? nr - (uint32_t)w * W : W);
         const uint32_t nbytes = (span + 15u) & ~15u;
+        const uint32_t lsum = store_lists(w);
+        uint32_t B;
+        const uint32_t pos = wg_excl_scan1(sh, lsum, &B);
+        place_lists(pos, B);
         wg_clear4(cnt, nbytes / 16);
         __syncthreads();
+        nblk += B;
         STAMP(t, SB_WINPRE);
         COUNT(t, SC_WIN, 1);
         COUNT(t, SC_BLK, B);
         fx_stream(t.fxent, plo, pstart, na, B, cnt, owner, dummy, sh);
         STAMP(t, SB_STREAM);
-        if (w >= 0) fx_collect_ordered(cnt, nbytes / 16, (uint32_t)thr, (uint32_t)w * W, sh, t.q1, (uint32_t)c.q_cap);
-        if (w < 0) {
+        if (w >= 0) {
+            fx_collect_ordered(cnt, nbytes / 16, (uint32_t)thr, (uint32_t)w * W, sh, t.q1, (uint32_t)c.q_cap);
+        } else {
             // pid counter >= activationThreshold: the segment's cell is predicted
             const uint32_t np = t.np;
             uint32_t* infP = t.infP;
@@ -993,13 +1021,20 @@ __device__ __forceinline__ uint32_t phase2_pass1(Tm& t, uint32_t qn, F emit) {
         }
     }
     for (uint32_t k = threadIdx.x; k < qn && !FROZEN; k += TM_NT) {
-        // learning scan: pool slots
-        const uint32_t slot = t.q1[k];
-        const uint32_t m = t.meta[slot];
+        // pool scan (collect_scan): the slot and the mask of its synapses onto
+        // active cells; connected ones = mask & the connected-synapse mask
+        const uint32_t slot = t.q1[k], amask = t.q2[k];
+        const uint32_t m = t.meta[slot], cm = t.conn[slot];
         const uint32_t cell = meta_cell(m), nsyn = meta_nsyn(m);
-        // meta + conn + used source rows + duty-cycle record read and written
-        nb += 4u + 12u + 8u;
+        // slot + mask + meta + conn + duty-cycle record read and written
+        nb += 4u + 4u + 4u + 4u + 12u + 8u;
+#ifdef HTM_PASS1_ROWS  // (A/B builds: the row read again, round 5)
+        (void)amask;
+        (void)cm;
         if (seg_connected_activity(t, slot, nsyn, nb) >= (uint32_t)c.act_thr)
+#else
+        if ((uint32_t)__popc(amask & cm & (nsyn >= 32u ? 0xFFFFFFFFu : (1u << nsyn) - 1u)) >= (uint32_t)c.act_thr)
+#endif
             atomicOr(&t.infP[cell >> 5], 1u << (cell & 31));
         emit(k, slot, cell, seg_dc_update(t.duty, slot, sh->lrn_iter, false));
     }
