@@ -106,7 +106,8 @@ struct htm_engine {
     bool flush_pending = false;       // ev_flushed not yet waited for by a step stream or the host
     int32_t flush_mode = 0;           // 0: flush stream beside the steps; 1: on the step stream
     int32_t flush_wg = FLUSH_WG;      // grid of a flush beside the steps
-    int32_t flush_prio = 0;           // 1: the flush stream at the lowest priority
+    int32_t flush_prio = 1;           // 1: the flush stream at the lowest priority (round 6: config 2
+                                      // 0.1548 -> 0.1529 ms/step same box, profiles/r06_ab/flush_stream/)
     size_t enc_cap = 0;               // steps SpBufs::enc_in holds (RDSE engines)
     bool conf_packed = false;         // a step kernel wrote colConfidence packed since the last densify
     bool lp2_pending = false;         // a learning step may have left its final learn phase 2 pending
