@@ -997,6 +997,7 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     if (int r = encode_rdse(e, d_values, n_steps, st)) return r;
     // deferred dutyCycle() writes: frozen lockstep launches (one step)
     const bool defer = frozen && n_steps == 1 && e->defer;
+    const int32_t cadence = e->flush_every ? e->flush_every : std::min(FLUSH_EVERY, e->dc.fx_dcap / 2);
     TmBufs tb = e->tm;
     if (defer) {
         if (int r = alloc_dlog(e)) return r;
@@ -1015,6 +1016,15 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
         tb.tm_only = 1;
         if (launch_ord_sort(e->dc, e->ord_est, e->ord, e->n, st))
             return htm_fail(HTM_E_HIP, "ord_sort launch");
+#ifndef HTM_FLUSH_AFTER_STEP
+        // a due flush of the deferred log starts here, after this step's SP
+        // kernel and sort: its workgroups and the TM launch's become ready
+        // together and the flush stream's low priority dispatches the launch's
+        // first (issued after the previous step's launch, the flush took the
+        // CUs during this SP kernel and sort and delayed the whole launch)
+        if (defer && e->defer_steps >= cadence)
+            if (int r = flush_async(e, st)) return r;
+#endif
         if (prof) HIP_TRY(hipEventRecord(ev[1], st));  // (the 256-thread TM launch's start)
     } else if (split) {
         if (launch_sp_step_ord(e->dc, e->sp, d_values, e->sp_learn, e->n, e->keep_overlaps, nullptr, nullptr, st))
@@ -1040,7 +1050,10 @@ static int run_fused(htm_engine* e, int32_t n_steps, const double* d_values, flo
     e->conf_packed = true;
     if (prof) HIP_TRY(hipEventRecord(ev[2], st));  // (the step kernel only: a flush is its own kernel)
     // (an explicit cadence, HTM_OPT_FLUSH_EVERY, is taken as given: past the ring the log fills)
-    if (defer && ++e->defer_steps >= (e->flush_every ? e->flush_every : std::min(FLUSH_EVERY, e->dc.fx_dcap / 2))) {
+    if (defer && ++e->defer_steps >= cadence) {
+#ifndef HTM_FLUSH_AFTER_STEP
+        if (ordered) return HTM_OK;  // (the next ordered step starts it before its TM launch)
+#endif
         int r = flush_async(e, st);  // beside the next steps
         if (r) return r;
     }
