@@ -661,7 +661,7 @@ def main():
                          "engine's own HIP stream, 1 on the step stream; auto: the engine's default")
     ap.add_argument("--flush-every", type=int, default=0,
                     help="HTM_OPT_FLUSH_EVERY: lockstep steps between the periodic deferred-write flushes (0: the "
-                         "engine default, 8)")
+                         "engine default, 4)")
     ap.add_argument("--ordered", choices=["on", "off"], default="on",
                     help="HTM_OPT_ORDERED: frozen lockstep steps run their TM steps heaviest first (on, the engine "
                          "default) or one fused SP+TM workgroup per stream in stream order (off); results identical")

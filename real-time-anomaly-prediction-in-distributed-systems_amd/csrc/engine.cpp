@@ -61,8 +61,12 @@ struct Region {
 // With ordered lockstep steps the TM launch's tail leaves more of the chip idle
 // and a wider flush fills it: 768 workgroups 0.1763 ms per step vs 256 0.1801
 // (512: 0.1764; 128-step regions), 20-step regions 0.1887 vs 0.1903
-// (profiles/r04_ab/flush_wg.txt)
-#define FLUSH_EVERY 8
+// (profiles/r04_ab/flush_wg.txt).  Round 6, the flush started beside the next
+// TM launch at the lowest stream priority: every 4 launches 0.1515 ms per step,
+// 6 0.1508, 8 0.1525, 2 0.1532 (2,324-step regions); 20-step regions 0.1618
+// (4) vs 0.1646 (8) -- a short region ends with at most 4 logged steps to
+// flush (profiles/r06_ab/flush_cadence/)
+#define FLUSH_EVERY 4
 #define FLUSH_WG 768
 
 struct htm_engine {
