@@ -634,6 +634,10 @@ def main():
                          "(same gpurun call): fills roofline.traffic")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the counter passes bench.py runs itself (N=1) to fill roofline.traffic")
+    ap.add_argument("--pmc-full", action="store_true",
+                    help="every counter pass on every leg: FETCH_SIZE (a cross-check of the request-size formula, "
+                         "calibrated in profiles/r02_final) and all three SQ passes on the learn_on and config5 legs "
+                         "(default: the config-2 kernel gets all SQ passes, the other legs SQ pass 1 only)")
     ap.add_argument("--no-learn-on", action="store_true",
                     help="config 2: skip the learn_on sub-record (config 3's learning streams, BASELINE's 'learn on')")
     ap.add_argument("--learn-streams", type=int, default=65536, help="learn_on: streams per GPU")
@@ -970,9 +974,9 @@ def main():
 # WRITE_SIZE 2): L2 memory-side requests by size, FETCH_SIZE, writes
 PMC_PASSES = {
     "pmc_rd": ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum"],
-    "pmc_fetch": ["FETCH_SIZE"],
     "pmc_wr": ["WRITE_SIZE", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"],
 }
+PMC_FETCH_PASS = {"pmc_fetch": ["FETCH_SIZE"]}  # (--pmc-full: traffic uses the request-size formula)
 PMC_L2_PASS = {"pmc_l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum"]}
 # where the waves' cycles go (SQ block: 8 counters per pass, SQ_WAVE_CYCLES in
 # each so every pass normalises itself): issuing / parked on s_waitcnt or
@@ -1042,10 +1046,15 @@ def self_pmc_passes(args, steps=128, learn_leg=False, c5_leg=False):
                 child += ["--" + k.replace("_", "-"), str(v)]
     env = dict(os.environ, TMPDIR="/tmp", HTM_BENCH_PMC_CHILD="1")
     passes = dict(PMC_PASSES)
+    full = getattr(args, "pmc_full", False)
+    if full:
+        passes.update(PMC_FETCH_PASS)
     if args.config == 4 and not learn_leg:
         passes.update(PMC_L2_PASS)  # the fleet's shared model is read from L2: its hit rate
-    if c5_leg:
-        passes.update({"pmc_sq1": PMC_SQ_PASSES["pmc_sq1"]})  # (one SQ pass: issue / wait fractions)
+    if (c5_leg or learn_leg) and not full:
+        # the sub-record legs: one SQ pass (issue / wait fractions) -- keeps the
+        # default run's 11 counter passes inside a few minutes
+        passes.update({"pmc_sq1": PMC_SQ_PASSES["pmc_sq1"]})
     else:
         passes.update(PMC_SQ_PASSES)
     for name, counters in passes.items():
