@@ -108,6 +108,7 @@ struct htm_engine {
     hipEvent_t ev_logged = nullptr;   // step stream: the snapshot of the log counters
     hipEvent_t ev_flushed = nullptr;  // fstream: the last enqueued flush is complete
     bool flush_pending = false;       // ev_flushed not yet waited for by a step stream or the host
+    int32_t final_split = 1;          // htm_flush's flush: jobs per (entry, rank window) (A/B knob HTM_FINAL_SPLIT)
     int32_t flush_mode = 0;           // 0: flush stream beside the steps; 1: on the step stream
     int32_t flush_wg = FLUSH_WG;      // grid of a flush beside the steps
     int32_t flush_prio = 1;           // 1: the flush stream at the lowest priority (round 6: config 2
@@ -576,6 +577,7 @@ static int create_uninit(const htm_config* cfg, int32_t n_streams, int32_t devic
     if (const char* env = ab_knob("HTM_FLUSH_WG")) e->flush_wg = std::max(0, std::atoi(env));         // A/B knob
     if (const char* env = ab_knob("HTM_ORDERED")) e->ordered = std::atoi(env) ? 1 : 0;               // A/B knob
     if (const char* env = ab_knob("HTM_FLUSH_PRIO")) e->flush_prio = std::atoi(env);                 // A/B knob
+    if (const char* env = ab_knob("HTM_FINAL_SPLIT")) e->final_split = std::atoi(env) ? 1 : 0;       // A/B knob
     int r = derive(*cfg, n_streams, budget, e->dc);
     if (r && !ab_knob("HTM_TM_LDS_BUDGET") && optin >= 78 * 1024) {
         // shapes whose fixed LDS state leaves no room at 3 workgroups per CU
@@ -815,7 +817,7 @@ static int flush_deferred(htm_engine* e, hipStream_t st) {
     }
     if (!e->tm.fx_dlog || !e->defer_steps) return HTM_OK;
     // (the caller waits on it: split per rank window, the latency of one window)
-    if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1, 1))
+    if (launch_tm_fx_flush(e->dc, e->tm, e->n, 0, st, 1, e->final_split))
         return htm_fail(HTM_E_HIP, "flush launch: %s", hipGetErrorString(hipGetLastError()));
     e->defer_steps = 0;
     return HTM_OK;

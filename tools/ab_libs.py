@@ -19,17 +19,18 @@ sys.path.insert(0, ROOT)
 import _pkg, bench
 rt = _pkg.load()
 N, K = int(os.environ.get("AB_STREAMS", "1024")), int(os.environ.get("AB_STEPS", "128"))
+R = int(os.environ.get("AB_REGIONS", "3"))
 d = np.load(os.path.join(ROOT, "tests", "golden", "model1_traces.npz"))
 train = [c for c, m in zip(d["train_cpu"], d["train_mem"]) if not (np.isnan(c) or np.isnan(m))][:2184]
 trace = d["test_cpu"].astype(np.float64)
 eng, _, _, _ = bench.trained_engine(rt, N, 72 * 1024, 0, train)
 eng.set_learning(False, False)
-vals = torch.tensor(bench.make_inputs(N, 0, N, 0, 16 + 3 * K, trace), device="cuda")
+vals = torch.tensor(bench.make_inputs(N, 0, N, 0, 16 + R * K, trace), device="cuda")
 for k in range(16):
     eng.step(vals[k])
 torch.cuda.synchronize()
 ts = []
-for r in range(3):
+for r in range(R):
     t0 = time.perf_counter()
     out = [eng.step(vals[16 + r * K + k]) for k in range(K)]
     eng.flush()
