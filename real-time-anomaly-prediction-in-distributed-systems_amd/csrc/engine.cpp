@@ -332,6 +332,13 @@ static int derive(const htm_config& c, int32_t n, size_t lds_budget, DevCfg& d) 
 #ifdef HTM_NO_LP2_DEFER  // (A/B builds)
     d.lp2_defer = 0;
 #endif
+    // the first block -> list map of a frozen window: written with the list
+    // starts (one barrier less) at Model-1's 12 cells per column (config 2
+    // 0.1546 -> 0.1531 ms/step); after their barrier at 32 (model.yaml fleet
+    // 23.31 -> 22.35 ms/step), where a thread's run of list starts is long
+    // (profiles/r06_ab/owner_map/)
+    d.fx_own_sep = d.K > 16 ? 1 : 0;
+    if (const char* env = ab_knob("HTM_FX_OWN_SEP")) d.fx_own_sep = std::atoi(env) ? 1 : 0;  // A/B knob
     if (const char* env = ab_knob("HTM_TM_FIN"))
         d.fin_mode = std::strcmp(env, "sorted") == 0 ? 1 : std::strcmp(env, "buckets") == 0 ? 0 : 2;
     // frozen-inference counter window: the union region holds the u8

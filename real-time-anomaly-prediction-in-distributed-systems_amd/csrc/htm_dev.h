@@ -71,6 +71,8 @@ struct DevCfg {
     int32_t q_lds_fx;                     // ... of a frozen phase 2 ranked in LDS (column u16 + dutyCycle f32
                                           // in the whole union region; more: the HBM scratch)
     int32_t lp2_defer;                    // learning steps defer their final learnPhase2 (tm_core.h lp2_finish)
+    int32_t fx_own_sep;                   // frozen windows: the first block -> list map built by fx_stream after
+                                          // the list starts' barrier (1), or by collect_frozen with them (0)
     int32_t fin_mode;                     // phase-2 tail: 0 column buckets (scans over all columns),
                                           // 1 bitonic key sort, 2 buckets over the nonzero-column bitmap
     int32_t max_act_cells;                // num_desired * K (frozen collection cell list)

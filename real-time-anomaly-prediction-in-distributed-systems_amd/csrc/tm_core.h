@@ -641,15 +641,15 @@ __device__ __forceinline__ void fx_owner_map(const uint32_t* pstart, uint32_t na
 // has read the map for its addresses -- LDS reads only: the loads stay in
 // flight), not before the next loads.  The first pass's map is the
 // caller's (collect_frozen writes it with the list starts, before its
-// barrier; -DHTM_OWNER_SEP builds it here, round 5).
+// barrier), or, `sep` (DevCfg::fx_own_sep), built here as in round 5.
 __device__ __forceinline__ void fx_stream(const uint4* ent, const uint32_t* plo, const uint32_t* pstart, uint32_t na,
-                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy,
+                                          uint32_t B, uint32_t* cnt, uint16_t* owner, uint32_t dummy, bool sep,
                                           TmSh* shp = nullptr) {
     if (B == 0) return;
-#ifdef HTM_OWNER_SEP
-    fx_owner_map(pstart, na, 0u, B < FX_OWN ? B : FX_OWN, owner);
-    __syncthreads();
-#endif
+    if (sep) {
+        fx_owner_map(pstart, na, 0u, B < FX_OWN ? B : FX_OWN, owner);
+        __syncthreads();
+    }
     STAMP_SH(shp, SB_OWNER);
     for (uint32_t lo = 0; lo < B; lo += FX_OWN) {
         const uint32_t hi = B - lo < FX_OWN ? B : lo + FX_OWN;
@@ -880,16 +880,17 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
     };
     // the lists' starts from this thread's exclusive prefix pos, and
     // fx_stream's first block -> list map from the starts in hand
+    const bool own_sep = c.fx_own_sep != 0;
     auto place_lists = [&](uint32_t pos, uint32_t B) {
         for (uint32_t j = 0; j < per; j++) {
             const uint32_t k = k0 + j;
             if (k >= na) break;
             const uint32_t n = pstart[k];
             pstart[k] = pos;
-#ifndef HTM_OWNER_SEP
-            const uint32_t e = pos + n < FX_OWN ? pos + n : FX_OWN;
-            for (uint32_t x = pos; x < e; x++) owner[x] = (uint16_t)k;
-#endif
+            if (!own_sep) {
+                const uint32_t e = pos + n < FX_OWN ? pos + n : FX_OWN;
+                for (uint32_t x = pos; x < e; x++) owner[x] = (uint16_t)k;
+            }
             pos += n;
         }
         if (threadIdx.x == 0) pstart[na] = B;
@@ -908,7 +909,7 @@ __device__ __forceinline__ void collect_frozen(Tm& t, int thr, int mode = FX_ALL
         STAMP(t, SB_WINPRE);
         COUNT(t, SC_WIN, 1);
         COUNT(t, SC_BLK, B);
-        fx_stream(t.fxent, plo, pstart, na, B, cnt, owner, dummy, sh);
+        fx_stream(t.fxent, plo, pstart, na, B, cnt, owner, dummy, own_sep, sh);
         STAMP(t, SB_STREAM);
         if (w >= 0) {
             fx_collect_ordered(cnt, nbytes / 16, (uint32_t)thr, (uint32_t)w * W, sh, t.q1, (uint32_t)c.q_cap);
