@@ -615,8 +615,8 @@ def main():
                     help="HIP events around every N-th launch of the timed region (HTM_OPT_PROFILE N; a timed "
                          "event record between dependent launches holds the queue ~12 us, so the roofline's "
                          "launch time is averaged over a sample: default every 5th -- prime to the deferred "
-                         "flush's 8-step cadence, whose following launch runs beside the flush: every 4th "
-                         "sampled that launch in half its samples, profiles/r05_ab/README.md)")
+                         "flush's cadence (round 5: 8 steps, whose following launch ran beside the flush: every 4th "
+                         "sampled that launch in half its samples, profiles/r05_ab/README.md; round 6: 6)")
     ap.add_argument("--mode", choices=["step", "run"], default="step",
                     help="step (default, the headline): lockstep -- one htm_step per step, every stream "
                          "advances one network.run(1) per step (north_star's real-time stepping); run: the K "

@@ -188,7 +188,7 @@ int htm_set_learning(htm_engine* eng, int32_t sp_learn, int32_t tm_learn);
                                    the TM steps heaviest first; results are identical.  0: one fused
                                    SP+TM workgroup per stream in stream order */
 #define HTM_OPT_FLUSH_EVERY 13  /* lockstep steps between the periodic flushes of the deferred dutyCycle()
-                                   writes (0: the default, 4, at most half the log ring); a cadence past
+                                   writes (0: the default, 6, at most half the log ring); a cadence past
                                    the ring makes the log fill, and a full log makes a step count its
                                    discarded phase 2s in full (results identical) */
 #define HTM_OPT_SPLIT_LEARN 14  /* 1 (default): a lockstep htm_step with TM learning on runs the SP kernel (its

@@ -64,9 +64,11 @@ struct Region {
 // (profiles/r04_ab/flush_wg.txt).  Round 6, the flush started beside the next
 // TM launch at the lowest stream priority: every 4 launches 0.1515 ms per step,
 // 6 0.1508, 8 0.1525, 2 0.1532 (2,324-step regions); 20-step regions 0.1618
-// (4) vs 0.1646 (8) -- a short region ends with at most 4 logged steps to
-// flush (profiles/r06_ab/flush_cadence/)
-#define FLUSH_EVERY 4
+// (4) vs 0.1646 (8) (profiles/r06_ab/flush_cadence/).  Measured again with
+// 12 20-step regions per process: 6 0.1586, 4 0.1592, 8 0.1599, 10 0.1630;
+// 2,324-step regions 6 0.1499 vs 4 0.1516 -- the end flush's time is not set
+// by how many logged steps it covers (profiles/r06_ab/final_flush/, flush_cadence/)
+#define FLUSH_EVERY 6
 #define FLUSH_WG 768
 
 struct htm_engine {
